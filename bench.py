@@ -1,0 +1,272 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X batched SHA-2 path (BASELINE.json metric).
+
+Default workload (BASELINE.json configs[1]): 1,048,576 x 1 KiB packets per
+GPU, SHA-256, device-resident.  One step = one launch of the hot path over
+the whole batch.  Multi-GPU: one process per GPU (torch.distributed.run),
+each rank hashes its own shard -- packets are independent, so there is no
+data-path collective; only the timing barrier and the max-over-ranks
+reduction talk across ranks.
+
+Prints ONE JSON line on rank 0.  --config selects another BASELINE config
+for DESIGN.md numbers (c3 mixed, c4 SHA-512, e2e host-memory path).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "SHA-256 digests/s over device-resident 1 KiB packets; HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, chip-level parameters
+# Vector-instruction issue peak: 256 CU x 4 SIMD, one wave64 VALU op per
+# 2 cycles per SIMD (SIMD-32), 2.4 GHz max clock (MI355X_MICROARCH.md).
+VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2
+
+CONFIGS = {
+    "c2": dict(alg=1, kind="fixed", n=1 << 20, length=1024,
+               workload="1M x 1 KiB packets, SHA-256, device-resident (BASELINE configs[1])"),
+    "c3": dict(alg=1, kind="mixed", n=1 << 20, length=None,
+               workload="1M x mixed {64,512,1500} B packets, SHA-256, length-binned (configs[2])"),
+    "c4": dict(alg=3, kind="fixed", n=1 << 20, length=1024,
+               workload="1M x 1 KiB packets, SHA-512, device-resident (configs[3])"),
+}
+DLEN = {1: 32, 2: 48, 3: 64}
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def make_inputs(cfg, dev, seed):
+    import torch
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    n = cfg["n"]
+    if cfg["kind"] == "fixed":
+        data = torch.randint(0, 256, (n * cfg["length"],), dtype=torch.uint8,
+                             device=dev, generator=g)
+        return dict(data=data, n=n, payload=n * cfg["length"])
+    choice = torch.tensor([64, 512, 1500], dtype=torch.int64, device=dev)
+    lens = choice[torch.randint(0, 3, (n,), device=dev, generator=g)]
+    offs = torch.zeros(n, dtype=torch.int64, device=dev)
+    offs[1:] = torch.cumsum(lens, 0)[:-1]
+    total = int(lens.sum().item())
+    data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev,
+                         generator=g)
+    return dict(data=data, n=n, offs=offs, lens=lens.to(torch.int32),
+                payload=total)
+
+
+def cpu_baseline(cfg):
+    """Oracle (clean-room C restatement of src/sha2.c, -O3) on host cores."""
+    import numpy as np
+    from oracle import oracle
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import synth
+    threads = min(16, len(os.sched_getaffinity(0)))
+    alg = cfg["alg"]
+    n = cfg["n"]
+    if cfg["kind"] == "fixed":
+        data = synth.fixed_batch(2, n, cfg["length"])
+        run = lambda t: oracle.batch(alg, data, stride=cfg["length"],  # noqa: E731
+                                     length=cfg["length"], n=n, nthreads=t)
+    else:
+        lens = synth.mixed_lengths(3, n)
+        data, offs = synth.packed(4, lens)
+        run = lambda t: oracle.batch(alg, data, offsets=offs, lens=lens,  # noqa: E731
+                                     nthreads=t)
+    run(threads)  # warm-up (page faults, thread start)
+    best = float("inf")
+    for _ in range(3):
+        t0 = time.perf_counter()
+        run(threads)
+        best = min(best, time.perf_counter() - t0)
+    return {"value": n / best, "unit": "digests/s", "cores": threads,
+            "kind": "port",
+            "sample": (f"the full {cfg['workload'].split(',')[0]} batch from host memory, "
+                       f"oracle/sha2_oracle.c (-O3, rolled transform like src/sha2.c:374-445) "
+                       f"on {threads} pthreads, best of 3 after a warm-up")}
+
+
+def load_pmc(config_name):
+    """Per-launch HBM traffic / VALU counts from the committed rocprofv3 PMC
+    summary (profiles/pmc_<config>.json, written by tools/pmc_summary.py)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config_name}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS) + ["e2e"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--unbinned", action="store_true",
+                    help="c3: hash in submission order (ablation)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from ilias_net2_amd import batch, _lib
+
+    ws, rank, local = dist_env()
+    if ws > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if ws > 1 else 0)
+    torch.cuda.set_device(dev)
+    if _lib.device_count() < 1:
+        raise SystemExit("no gfx950 device visible to libnet2_sha2.so")
+
+    if args.config == "e2e":
+        return run_e2e(args, ws, rank, dev)
+
+    cfg = CONFIGS[args.config]
+    inp = make_inputs(cfg, dev, seed=2 + rank)
+    n, alg = inp["n"], cfg["alg"]
+    out = torch.empty((n, DLEN[alg]), dtype=torch.uint8, device=dev)
+    ws_buf = batch.var_workspace(n, dev) if cfg["kind"] == "mixed" else None
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        if cfg["kind"] == "fixed":
+            batch.digest_fixed(alg, inp["data"], cfg["length"], cfg["length"],
+                               n, out=out, stream=stream)
+        else:
+            batch.digest_var(alg, inp["data"], inp["offs"], inp["lens"],
+                             out=out, workspace=ws_buf,
+                             binned=not args.unbinned, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    # HIP events on the stream the kernels are launched on.
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        step()
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    if ws > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    launch_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+
+    if ws > 1:
+        t = torch.tensor([elapsed, launch_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, launch_ms = float(t[0]), float(t[1])
+
+    ms_per_step = elapsed * 1e3 / args.steps
+    total_digests = n * ws
+    value = total_digests / (ms_per_step / 1e3)
+
+    # Roofline of the dominant kernel: algorithmic bytes = payload read +
+    # digests written (+ 12 B/packet offsets+lens for the mixed layout),
+    # per launch, over the event-timed launch duration.
+    per_launch = inp["payload"] + n * DLEN[alg] + (12 * n if cfg["kind"] == "mixed" else 0)
+    achieved = per_launch / (launch_ms / 1e3) / 1e9
+    pmc = load_pmc(args.config)
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+            "kernel_ms": round(launch_ms, 4),
+            "algorithmic_bytes_per_launch": per_launch}
+    valu = None
+    if pmc and pmc.get("valu_wave_instr_per_launch"):
+        rate = pmc["valu_wave_instr_per_launch"] / (launch_ms / 1e3)
+        valu = {"bound": "valu", "achieved": round(rate / 1e12, 4),
+                "peak": round(VALU_PEAK_WAVE_INSTR / 1e12, 4),
+                "unit": "T wave64-VALU-instr/s",
+                "frac": round(rate / VALU_PEAK_WAVE_INSTR, 4),
+                "source": "rocprofv3 SQ_INSTS_VALU, profiles/pmc_%s.json" % args.config}
+
+    line = {
+        "metric": METRIC if args.config == "c2" else
+        f"{'SHA-512' if alg == 3 else 'SHA-256'} digests/s, {cfg['workload']}",
+        "value": round(value, 1), "unit": "digests/s", "n_gpus": ws,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32" if alg == 1 else "u64",
+        "data": "synthetic: uniform random bytes (torch.randint, seed 2+rank), resident in HBM before timing",
+        "config": {"workload": cfg["workload"] + (" [unbinned]" if args.unbinned else ""),
+                   "packets_per_gpu": n, "alg": "SHA256" if alg == 1 else "SHA512",
+                   "payload_bytes_per_gpu": inp["payload"],
+                   "parallelism": f"{ws} independent shards, no collective"},
+        "roofline": roof,
+    }
+    if valu:
+        line["roofline_valu"] = valu
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(cfg)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+def run_e2e(args, ws, rank, dev):
+    """Config 5 shape: host memory -> pinned H2D -> kernel -> D2H -> host,
+    through net2_sha2_batch on this rank's device (PCIe-inclusive rate)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from ilias_net2_amd import _lib
+    n, length = 1 << 20, 1024
+    host = torch.randint(0, 256, (n * length,), dtype=torch.uint8).pin_memory()
+    outp = torch.empty((n, 32), dtype=torch.uint8).pin_memory()
+    L = _lib.lib()
+
+    def step():
+        _lib.check(L.net2_sha2_batch(1, host.data_ptr(), None, None, length,
+                                     length, n, outp.data_ptr(), 1))
+    for _ in range(args.warmup):
+        step()
+    if ws > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if ws > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t[0])
+    ms = el * 1e3 / args.steps
+    if rank == 0:
+        print(json.dumps({
+            "metric": "SHA-256 digests/s, 1 KiB packets from pinned host memory, end to end (H2D + kernel + D2H)",
+            "value": round(n * ws / (ms / 1e3), 1), "unit": "digests/s", "n_gpus": ws,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u32", "data": "synthetic random bytes in pinned host memory",
+            "config": {"workload": "1M x 1 KiB per GPU, host -> GPU -> host via net2_sha2_batch",
+                       "h2d_GBps": round(n * length / (ms / 1e3) / 1e9, 2)}}), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
+    del np
+
+
+if __name__ == "__main__":
+    main()

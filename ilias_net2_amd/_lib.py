@@ -1,0 +1,109 @@
+"""ctypes binding of libnet2_sha2.so, the C-ABI of the MI355X SHA-2 path.
+
+The binding declares exactly the entry points of include/net2/sha2_batch.h and
+include/net2/hash.h.  Loading is strict: if the shared library is missing the
+import of any compute helper raises, there is no Python or CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import errno
+import os
+
+LIB_NAME = "libnet2_sha2.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+# Registry rows (include/net2/sha2_batch.h, include/net2/hash.h).
+NIL, SHA256, SHA384, SHA512 = 0, 1, 2, 3
+HMAC_SHA256, HMAC_SHA384, HMAC_SHA512 = 4, 5, 6
+DIGEST_LEN = {SHA256: 32, SHA384: 48, SHA512: 64,
+              HMAC_SHA256: 32, HMAC_SHA384: 48, HMAC_SHA512: 64}
+BLOCK_LEN = {SHA256: 64, SHA384: 128, SHA512: 128}
+
+
+class Net2Error(OSError):
+    """A non-zero errno-style return from the C ABI."""
+
+
+class IOVec(ctypes.Structure):
+    _fields_ = [("iov_base", ctypes.c_void_p), ("iov_len", ctypes.c_size_t)]
+
+
+_c_u64p = ctypes.POINTER(ctypes.c_uint64)
+_c_u32p = ctypes.POINTER(ctypes.c_uint32)
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "net2_sha2_abi_version": (ctypes.c_int, []),
+    "net2_sha2_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "net2_sha2_last_hip_error": (ctypes.c_int, []),
+    "net2_sha2_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "net2_sha2_dev_fixed": (ctypes.c_int, [
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+        ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+    "net2_sha2_dev_var": (ctypes.c_int, [
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+        ctypes.c_void_p]),
+    "net2_sha2_dev_var_workspace": (ctypes.c_size_t, [ctypes.c_uint64]),
+    "net2_sha2_batch": (ctypes.c_int, [
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
+        ctypes.c_int]),
+    "net2_hash_getname": (ctypes.c_char_p, [ctypes.c_int]),
+    "net2_hash_findname": (ctypes.c_int, [ctypes.c_char_p]),
+    "net2_hash_gethashlen": (ctypes.c_int, [ctypes.c_int]),
+    "net2_hash_getkeylen": (ctypes.c_int, [ctypes.c_int]),
+    "net2_hashctx_hashiov": (ctypes.c_int, [
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+        ctypes.POINTER(IOVec), ctypes.c_size_t, ctypes.c_void_p,
+        ctypes.c_size_t]),
+    "net2_hmac_dev": (ctypes.c_int, [
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+        ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+}
+DATA_SYMBOLS = ("net2_hashmax",)
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """The loaded C ABI; raises if the HIP library was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` "
+                "(there is no CPU fallback for the SHA-2 path)")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def strerror(rc: int) -> str:
+    return lib().net2_sha2_strerror(rc).decode()
+
+
+def check(rc: int, what: str = "") -> None:
+    """Raise Net2Error for a non-zero return code."""
+    if rc != 0:
+        msg = strerror(rc)
+        if rc == errno.EIO:
+            msg += f" (hip error {lib().net2_sha2_last_hip_error()})"
+        raise Net2Error(rc, f"{what}: {msg}" if what else msg)
+
+
+def hashmax() -> int:
+    return ctypes.c_int.in_dll(lib(), "net2_hashmax").value
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = lib().net2_sha2_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0

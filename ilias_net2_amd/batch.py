@@ -1,0 +1,98 @@
+"""Batched digests over device-resident or host packets (torch / numpy glue).
+
+PyTorch is plumbing here: it owns device memory and streams; the digests come
+from the HIP kernels behind ``net2_sha2_dev_fixed`` / ``net2_sha2_dev_var`` /
+``net2_sha2_batch`` (include/net2/sha2_batch.h).  The batched entry is what
+``net2_signature_create`` / ``_validate`` (types/signature.n2t:92,147) and
+``net2_signctx_fingerprint`` (src/sign.c:298-307) reduce to when many payloads
+are hashed at once.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import DIGEST_LEN, check
+
+
+def _stream_ptr(stream) -> Optional[int]:
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def digest_fixed(alg: int, data, stride: int, length: int, n: int, out=None,
+                 stream=None):
+    """Digests of n packets data[i*stride : i*stride+length] (uint8 CUDA tensor).
+
+    Returns an (n, hashlen) uint8 tensor on the same device.  Asynchronous on
+    ``stream`` (default: torch's current stream)."""
+    import torch
+    dl = DIGEST_LEN[alg]
+    if out is None:
+        out = torch.empty((n, dl), dtype=torch.uint8, device=data.device)
+    if n and data.numel() < (n - 1) * stride + length:
+        raise ValueError("data tensor too small for n packets")
+    rc = _lib.lib().net2_sha2_dev_fixed(alg, data.data_ptr(), stride, length,
+                                        n, out.data_ptr(), _stream_ptr(stream))
+    check(rc, "net2_sha2_dev_fixed")
+    return out
+
+
+def var_workspace(n: int, device):
+    import torch
+    nbytes = _lib.lib().net2_sha2_dev_var_workspace(n)
+    return torch.empty(((nbytes + 3) // 4,), dtype=torch.int32, device=device)
+
+
+def digest_var(alg: int, data, offsets, lens, out=None, workspace=None,
+               binned: bool = True, stream=None):
+    """Digests of packets data[offsets[i] : offsets[i]+lens[i]].
+
+    data: uint8 CUDA tensor; offsets: int64 CUDA tensor; lens: int32 CUDA
+    tensor.  binned=True sorts by block count on the device first."""
+    import torch
+    n = int(offsets.numel())
+    dl = DIGEST_LEN[alg]
+    if out is None:
+        out = torch.empty((n, dl), dtype=torch.uint8, device=data.device)
+    ws_ptr, ws_bytes = None, 0
+    if binned and n:
+        if workspace is None:
+            workspace = var_workspace(n, data.device)
+        ws_ptr, ws_bytes = workspace.data_ptr(), workspace.numel() * 4
+    rc = _lib.lib().net2_sha2_dev_var(alg, data.data_ptr(), offsets.data_ptr(),
+                                      lens.data_ptr(), n, out.data_ptr(),
+                                      ws_ptr, ws_bytes, _stream_ptr(stream))
+    check(rc, "net2_sha2_dev_var")
+    return out
+
+
+def _np_ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def digest_host(alg: int, data: np.ndarray, offsets: Optional[np.ndarray] = None,
+                lens: Optional[np.ndarray] = None, stride: int = 0,
+                length: int = 0, n: Optional[int] = None,
+                max_devices: int = 0) -> np.ndarray:
+    """End-to-end batch from host memory (numpy) -> host digests (numpy)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    if offsets is not None:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        n = len(offsets)
+    elif n is None:
+        n = (len(data) // stride) if stride else 0
+    out = np.empty((n, DIGEST_LEN[alg]), dtype=np.uint8)
+    rc = _lib.lib().net2_sha2_batch(alg, _np_ptr(data), _np_ptr(offsets),
+                                    _np_ptr(lens), stride, length, n,
+                                    _np_ptr(out), max_devices)
+    check(rc, "net2_sha2_batch")
+    return out

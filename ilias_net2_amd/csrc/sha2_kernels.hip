@@ -1,0 +1,552 @@
+/*
+ * sha2_kernels.hip -- batched SHA-256/384/512 digests for gfx950 (MI355X).
+ *
+ * The reference hashes one payload at a time on a host thread:
+ * SHA{256,512}Init -> Update (per iovec) -> Final (src/sha2.c:280-563,
+ * :566-919), called from net2_signature_create/validate
+ * (types/signature.n2t:92,147) and net2_signctx_fingerprint
+ * (src/sign.c:298-307).  Here one wavefront lane owns one packet and runs
+ * Init/Update/Pad/Final for it entirely in registers; a launch covers a whole
+ * batch of independent packets.
+ *
+ * Layouts (device memory):
+ *   fixed  : packet i = base[i * stride .. i * stride + len)
+ *   var    : packet i = base[offsets[i] .. offsets[i] + lens[i])
+ *   digests: digest i at out + i * digest_len (32 / 48 / 64 bytes)
+ * Variable-length batches are length-binned first (bin_* kernels below) so
+ * that the lanes of a wave share a block count: an unbinned {64,512,1500} B
+ * mix runs every wave at the 24-block worst case, binned at the average.
+ *
+ * The block loop is VALU-bound (~1,400 integer ops per 64-byte SHA-256
+ * block), so the memory side only has to keep loads in flight: each lane
+ * prefetches block k+1 while compressing block k.
+ */
+#include "sha2_device.h"
+#include "sha2_launch.h"
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace net2 {
+namespace dev {
+
+/* ---- hash traits ------------------------------------------------------ */
+
+struct Sha256 {
+	typedef uint32_t word;
+	static constexpr int BLOCK = 64;	/* bytes per block */
+	static constexpr int NW32 = 16;		/* 32-bit words per block */
+	static constexpr int LENBYTES = 8;	/* trailing length field */
+	static constexpr int DLEN = 32;
+	typedef uint32_t State[8];
+
+	__device__ __forceinline__ static void init(State &st, int)
+	{
+#pragma unroll
+		for (int i = 0; i < 8; i++)
+			st[i] = IV256[i];
+	}
+	__device__ __forceinline__ static void compress(State &st,
+	    uint32_t (&b)[16])
+	{
+		compress256(st, b);
+	}
+	/* Store state big-endian (src/sha2.c:553-557) as 32-bit words. */
+	__device__ __forceinline__ static void out_words(const State &st,
+	    uint32_t (&o)[16], int)
+	{
+#pragma unroll
+		for (int i = 0; i < 8; i++)
+			o[i] = bswap32(st[i]);
+	}
+};
+
+struct Sha512 {
+	typedef uint64_t word;
+	static constexpr int BLOCK = 128;
+	static constexpr int NW32 = 32;
+	static constexpr int LENBYTES = 16;
+	static constexpr int DLEN = 64;		/* 48 for SHA-384 */
+	typedef uint64_t State[8];
+
+	__device__ __forceinline__ static void init(State &st, int is384)
+	{
+#pragma unroll
+		for (int i = 0; i < 8; i++)
+			st[i] = is384 ? IV384[i] : IV512[i];
+	}
+	__device__ __forceinline__ static void compress(State &st,
+	    uint32_t (&b)[32])
+	{
+		uint64_t w[16];
+#pragma unroll
+		for (int i = 0; i < 16; i++)
+			w[i] = mk64(b[2 * i + 1], b[2 * i]);
+		compress512(st, w);
+	}
+	__device__ __forceinline__ static void out_words(const State &st,
+	    uint32_t (&o)[16], int)
+	{
+#pragma unroll
+		for (int i = 0; i < 8; i++) {
+			o[2 * i] = bswap32(hi32(st[i]));
+			o[2 * i + 1] = bswap32(lo32(st[i]));
+		}
+	}
+};
+
+/* ---- message loading ------------------------------------------------- */
+
+/*
+ * Address modes.  A16: every packet start in the wave is 16-byte aligned, a
+ * block is NW32/4 global_load_dwordx4.  A1: arbitrary byte alignment; the
+ * block is read as NW32 + 1 naturally aligned dwords (the extra one only
+ * when misaligned, so no dword outside the packet's own bytes is touched)
+ * and re-aligned with v_alignbyte_b32.
+ */
+enum { AMODE_A16 = 0, AMODE_A1 = 1 };
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int NW32>
+struct Raw {
+	uint32_t d[NW32 + 1];
+};
+
+template <int NW32, int AMODE>
+__device__ __forceinline__ void issue_block(const uint8_t *p, Raw<NW32> &r)
+{
+	if (AMODE == AMODE_A16) {
+		const u32x4 *q = reinterpret_cast<const u32x4 *>(p);
+#pragma unroll
+		for (int i = 0; i < NW32 / 4; i++) {
+			u32x4 v = q[i];
+			r.d[4 * i] = v.x;
+			r.d[4 * i + 1] = v.y;
+			r.d[4 * i + 2] = v.z;
+			r.d[4 * i + 3] = v.w;
+		}
+	} else {
+		uintptr_t a = reinterpret_cast<uintptr_t>(p);
+		const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+#pragma unroll
+		for (int i = 0; i < NW32; i++)
+			r.d[i] = q[i];
+		r.d[NW32] = (a & 3) ? q[NW32] : 0u;
+	}
+}
+
+/* Raw little-endian dwords -> big-endian message words. */
+template <int NW32, int AMODE>
+__device__ __forceinline__ void finish_block(const uint8_t *p,
+    const Raw<NW32> &r, uint32_t (&w)[NW32])
+{
+	if (AMODE == AMODE_A16) {
+#pragma unroll
+		for (int i = 0; i < NW32; i++)
+			w[i] = bswap32(r.d[i]);
+	} else {
+		uint32_t sh = (uint32_t)reinterpret_cast<uintptr_t>(p) & 3;
+#pragma unroll
+		for (int i = 0; i < NW32; i++)
+			w[i] = bswap32(__builtin_amdgcn_alignbyte(r.d[i + 1],
+			    r.d[i], sh));
+	}
+}
+
+/*
+ * The last data bytes q[0 .. rem) (rem < BLOCK) followed by the 0x80
+ * terminator and zero fill, as big-endian words (the buffer SHA256Pad /
+ * SHA512Pad build, src/sha2.c:495-526 / :784-812).  Only dwords that hold
+ * packet bytes are read.
+ */
+template <int NW32>
+__device__ __forceinline__ void tail_block(const uint8_t *q, uint32_t rem,
+    uint32_t (&w)[NW32])
+{
+	uintptr_t a = reinterpret_cast<uintptr_t>(q);
+	uint32_t sh = (uint32_t)a & 3;
+	const uint32_t *al = reinterpret_cast<const uint32_t *>(a - sh);
+	uint32_t d[NW32 + 1];
+#pragma unroll
+	for (int j = 0; j <= NW32; j++)
+		d[j] = (uint32_t)(4 * j) < sh + rem ? al[j] : 0u;
+#pragma unroll
+	for (int i = 0; i < NW32; i++) {
+		uint32_t x = bswap32(__builtin_amdgcn_alignbyte(d[i + 1], d[i],
+		    sh));
+		int kk = (int)rem - 4 * i;	/* message bytes in this word */
+		if (kk < 4) {
+			uint32_t keep = kk > 0 ? ~(0xffffffffu >> (8 * kk)) : 0u;
+			uint32_t mark = kk >= 0 ? 0x80000000u >> (8 * kk) : 0u;
+			x = (x & keep) | mark;
+		}
+		w[i] = x;
+	}
+}
+
+/* Digest store: 16-byte vector stores when aligned, bytes otherwise. */
+template <int DLEN>
+__device__ __forceinline__ void store_digest(uint8_t *o, const uint32_t (&v)[16])
+{
+	if ((reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+		uint4 *q = reinterpret_cast<uint4 *>(o);
+#pragma unroll
+		for (int i = 0; i < DLEN / 16; i++)
+			q[i] = make_uint4(v[4 * i], v[4 * i + 1], v[4 * i + 2],
+			    v[4 * i + 3]);
+	} else {
+#pragma unroll
+		for (int i = 0; i < DLEN / 4; i++) {
+			uint32_t x = v[i];
+			o[4 * i] = (uint8_t)x;
+			o[4 * i + 1] = (uint8_t)(x >> 8);
+			o[4 * i + 2] = (uint8_t)(x >> 16);
+			o[4 * i + 3] = (uint8_t)(x >> 24);
+		}
+	}
+}
+
+/*
+ * Whole-message digest for one lane.  nfull full blocks stream from p with
+ * a one-block prefetch; then the generic tail (data remainder + 0x80 +
+ * length, one or two blocks), or -- when the caller knows every message of
+ * the launch is a multiple of the block size -- the constant padding block
+ * whose K[t] + W[t] schedule the host precomputed (kw).
+ */
+template <class H, int AMODE, bool PADCONST>
+__device__ __forceinline__ void digest_one(const uint8_t *p, uint32_t len,
+    int is384, const typename H::word *kw, typename H::State &st)
+{
+	constexpr int NW32 = H::NW32;
+	const uint32_t nfull = len / H::BLOCK;
+	const uint32_t rem = len % H::BLOCK;
+
+	H::init(st, is384);
+
+	Raw<NW32> cur;
+	if (nfull > 0)
+		issue_block<NW32, AMODE>(p, cur);
+	for (uint32_t k = 0; k < nfull; k++) {
+		const uint8_t *bp = p + (size_t)k * H::BLOCK;
+		Raw<NW32> nxt;
+		if (k + 1 < nfull)
+			issue_block<NW32, AMODE>(bp + H::BLOCK, nxt);
+		uint32_t w[NW32];
+		finish_block<NW32, AMODE>(bp, cur, w);
+		H::compress(st, w);
+		cur = nxt;
+	}
+
+	/* Message length in bits, big-endian, at the end of the last block. */
+	const uint64_t bits = (uint64_t)len << 3;
+	if (PADCONST) {
+		if (sizeof(typename H::word) == 4)
+			compress256_kw(*reinterpret_cast<uint32_t(*)[8]>(&st),
+			    reinterpret_cast<const uint32_t *>(kw));
+		else
+			compress512_kw(*reinterpret_cast<uint64_t(*)[8]>(&st),
+			    reinterpret_cast<const uint64_t *>(kw));
+		return;
+	}
+	uint32_t w[NW32];
+	tail_block<NW32>(p + (size_t)nfull * H::BLOCK, rem, w);
+	if (rem >= (uint32_t)(H::BLOCK - H::LENBYTES)) {
+		/* No room for the length: this block, then a zero block. */
+		H::compress(st, w);
+#pragma unroll
+		for (int i = 0; i < NW32; i++)
+			w[i] = 0;
+	}
+	w[NW32 - 2] = (uint32_t)(bits >> 32);
+	w[NW32 - 1] = (uint32_t)bits;
+	H::compress(st, w);
+}
+
+/* Constant-pad schedule passed by value (kernarg -> SGPRs). */
+template <class W>
+struct PadKW {
+	W kw[sizeof(W) == 4 ? 64 : 80];
+};
+
+template <class H, int AMODE, bool PADCONST>
+__global__ __launch_bounds__(256) void fixed_kernel(const uint8_t *__restrict__ base,
+    uint64_t stride, uint32_t len, uint64_t n, uint8_t *__restrict__ out,
+    uint32_t dlen, int is384, PadKW<typename H::word> pad)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n)
+		return;
+	typename H::State st;
+	digest_one<H, AMODE, PADCONST>(base + i * stride, len, is384, pad.kw,
+	    st);
+	uint32_t o[16];
+	H::out_words(st, o, is384);
+	if (dlen == 48)
+		store_digest<48>(out + i * 48, o);
+	else
+		store_digest<H::DLEN>(out + i * H::DLEN, o);
+}
+
+/*
+ * Variable-length packets, visited in binned order: lane g hashes packet
+ * perm[g] (perm == NULL: identity).  The address mode is chosen per wave:
+ * if every lane's packet start is 16-byte aligned the wave takes the vector
+ * load path, else the byte-aligned one.
+ */
+template <class H>
+__global__ __launch_bounds__(256) void var_kernel(const uint8_t *__restrict__ base,
+    const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
+    const uint32_t *__restrict__ perm, uint64_t n, uint8_t *__restrict__ out,
+    uint32_t dlen, int is384)
+{
+	const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	const bool live = g < n;
+	const uint64_t i = live ? (perm ? (uint64_t)perm[g] : g) : 0;
+	const uint8_t *p = base + (live ? offsets[i] : 0);
+	const uint32_t len = live ? lens[i] : 0;
+	typename H::State st;
+
+	if (__all((reinterpret_cast<uintptr_t>(p) & 15) == 0))
+		digest_one<H, AMODE_A16, false>(p, len, is384, nullptr, st);
+	else
+		digest_one<H, AMODE_A1, false>(p, len, is384, nullptr, st);
+	if (!live)
+		return;
+	uint32_t o[16];
+	H::out_words(st, o, is384);
+	if (dlen == 48)
+		store_digest<48>(out + i * 48, o);
+	else
+		store_digest<H::DLEN>(out + i * H::DLEN, o);
+}
+
+/* ---- length binning (counting sort by block count, longest first) ---- */
+
+__device__ __forceinline__ uint32_t bin_of(uint32_t len, int blk_shift,
+    int lenbytes, uint32_t nbins)
+{
+	/* total compressions the message needs, including padding */
+	uint64_t nb = (((uint64_t)len + lenbytes + 1 + (1u << blk_shift) - 1) >>
+	    blk_shift);
+	uint32_t b = nb >= nbins ? nbins - 1 : (uint32_t)nb;
+	return nbins - 1 - b;	/* descending block count */
+}
+
+__global__ __launch_bounds__(256) void bin_count_kernel(
+    const uint32_t *__restrict__ lens, uint64_t n, int blk_shift,
+    int lenbytes, uint32_t *__restrict__ hist)
+{
+	__shared__ uint32_t lh[NET2_SHA2_NBINS];
+	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
+		lh[b] = 0;
+	__syncthreads();
+	const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+	for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+	    i += stride)
+		atomicAdd(&lh[bin_of(lens[i], blk_shift, lenbytes,
+		    NET2_SHA2_NBINS)], 1u);
+	__syncthreads();
+	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
+		if (lh[b] != 0)
+			atomicAdd(&hist[b], lh[b]);
+}
+
+/* Exclusive scan of the histogram into bin cursors; one 1024-thread block. */
+__global__ __launch_bounds__(1024) void bin_scan_kernel(
+    const uint32_t *__restrict__ hist, uint32_t *__restrict__ cursor)
+{
+	__shared__ uint32_t part[1024];
+	constexpr int PER = NET2_SHA2_NBINS / 1024;
+	uint32_t loc[PER], s = 0;
+#pragma unroll
+	for (int j = 0; j < PER; j++) {
+		loc[j] = s;
+		s += hist[threadIdx.x * PER + j];
+	}
+	part[threadIdx.x] = s;
+	__syncthreads();
+	for (int off = 1; off < 1024; off <<= 1) {
+		uint32_t v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0;
+		__syncthreads();
+		part[threadIdx.x] += v;
+		__syncthreads();
+	}
+	uint32_t base = threadIdx.x ? part[threadIdx.x - 1] : 0;
+#pragma unroll
+	for (int j = 0; j < PER; j++)
+		cursor[threadIdx.x * PER + j] = base + loc[j];
+}
+
+/*
+ * Scatter packet indices to their bin.  Each block ranks its own packets
+ * per bin in LDS, claims one range per touched bin with a single global
+ * atomic, then writes perm[].  Order inside a bin is unspecified; digests
+ * are stored by packet index, so the output does not depend on it.
+ */
+__global__ __launch_bounds__(256) void bin_scatter_kernel(
+    const uint32_t *__restrict__ lens, uint64_t n, int blk_shift,
+    int lenbytes, uint32_t *__restrict__ cursor, uint32_t *__restrict__ perm)
+{
+	__shared__ uint32_t cnt[NET2_SHA2_NBINS];
+	__shared__ uint32_t basep[NET2_SHA2_NBINS];
+	const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+	for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n;
+	    i0 += stride) {
+		for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
+			cnt[b] = 0;
+		__syncthreads();
+		const uint64_t i = i0 + threadIdx.x;
+		uint32_t bin = 0, rank = 0;
+		if (i < n) {
+			bin = bin_of(lens[i], blk_shift, lenbytes,
+			    NET2_SHA2_NBINS);
+			rank = atomicAdd(&cnt[bin], 1u);
+		}
+		__syncthreads();
+		for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
+			if (cnt[b] != 0)
+				basep[b] = atomicAdd(&cursor[b], cnt[b]);
+		__syncthreads();
+		if (i < n)
+			perm[basep[bin] + rank] = (uint32_t)i;
+		__syncthreads();
+	}
+}
+
+/* ---- host-side constant pad schedule ---------------------------------- */
+
+static inline uint32_t h_ror32(uint32_t x, int n)
+{
+	return (x >> n) | (x << (32 - n));
+}
+static inline uint64_t h_ror64(uint64_t x, int n)
+{
+	return (x >> n) | (x << (64 - n));
+}
+
+/* Pad block of a message whose length is a multiple of the block size. */
+static void pad_kw256(uint64_t bits, PadKW<uint32_t> &p)
+{
+	uint32_t w[64] = { 0 };
+	w[0] = 0x80000000u;
+	w[14] = (uint32_t)(bits >> 32);
+	w[15] = (uint32_t)bits;
+	for (int t = 16; t < 64; t++) {
+		uint32_t s0 = h_ror32(w[t - 15], 7) ^ h_ror32(w[t - 15], 18) ^
+		    (w[t - 15] >> 3);
+		uint32_t s1 = h_ror32(w[t - 2], 17) ^ h_ror32(w[t - 2], 19) ^
+		    (w[t - 2] >> 10);
+		w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+	}
+	for (int t = 0; t < 64; t++)
+		p.kw[t] = K256[t] + w[t];
+}
+
+static void pad_kw512(uint64_t bits, PadKW<uint64_t> &p)
+{
+	uint64_t w[80] = { 0 };
+	w[0] = 0x8000000000000000ull;
+	w[15] = bits;	/* w[14] = high 64 bits of the 128-bit count = 0 */
+	for (int t = 16; t < 80; t++) {
+		uint64_t s0 = h_ror64(w[t - 15], 1) ^ h_ror64(w[t - 15], 8) ^
+		    (w[t - 15] >> 7);
+		uint64_t s1 = h_ror64(w[t - 2], 19) ^ h_ror64(w[t - 2], 61) ^
+		    (w[t - 2] >> 6);
+		w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+	}
+	for (int t = 0; t < 80; t++)
+		p.kw[t] = K512[t] + w[t];
+}
+
+} /* namespace dev */
+} /* namespace net2 */
+
+/* ---- launch wrappers (C++ linkage, used by the C-ABI shim) ------------ */
+
+using namespace net2::dev;
+
+static inline unsigned grid_for(uint64_t n)
+{
+	return (unsigned)((n + 255) / 256);
+}
+
+hipError_t net2_launch_fixed(int alg, const uint8_t *base, uint64_t stride,
+    uint32_t len, uint64_t n, uint8_t *out, hipStream_t s)
+{
+	const bool a16 = ((reinterpret_cast<uintptr_t>(base) | stride) & 15) == 0;
+	const unsigned grid = grid_for(n);
+	if (n == 0)
+		return hipSuccess;
+	if (alg == NET2_ALG_SHA256) {
+		PadKW<uint32_t> pad;
+		const bool padc = len % 64 == 0;
+		if (padc)
+			pad_kw256((uint64_t)len << 3, pad);
+		if (a16 && padc)
+			fixed_kernel<Sha256, AMODE_A16, true><<<grid, 256, 0, s>>>(
+			    base, stride, len, n, out, 32, 0, pad);
+		else if (a16)
+			fixed_kernel<Sha256, AMODE_A16, false><<<grid, 256, 0, s>>>(
+			    base, stride, len, n, out, 32, 0, pad);
+		else
+			fixed_kernel<Sha256, AMODE_A1, false><<<grid, 256, 0, s>>>(
+			    base, stride, len, n, out, 32, 0, pad);
+	} else {
+		const int is384 = alg == NET2_ALG_SHA384;
+		const uint32_t dlen = is384 ? 48 : 64;
+		PadKW<uint64_t> pad;
+		const bool padc = len % 128 == 0;
+		if (padc)
+			pad_kw512((uint64_t)len << 3, pad);
+		if (a16 && padc)
+			fixed_kernel<Sha512, AMODE_A16, true><<<grid, 256, 0, s>>>(
+			    base, stride, len, n, out, dlen, is384, pad);
+		else if (a16)
+			fixed_kernel<Sha512, AMODE_A16, false><<<grid, 256, 0, s>>>(
+			    base, stride, len, n, out, dlen, is384, pad);
+		else
+			fixed_kernel<Sha512, AMODE_A1, false><<<grid, 256, 0, s>>>(
+			    base, stride, len, n, out, dlen, is384, pad);
+	}
+	return hipGetLastError();
+}
+
+hipError_t net2_launch_var(int alg, const uint8_t *base,
+    const uint64_t *offsets, const uint32_t *lens, uint64_t n, uint8_t *out,
+    uint32_t *ws, hipStream_t s)
+{
+	if (n == 0)
+		return hipSuccess;
+	const bool s256 = alg == NET2_ALG_SHA256;
+	const int blk_shift = s256 ? 6 : 7;
+	const int lenbytes = s256 ? 8 : 16;
+	const int is384 = alg == NET2_ALG_SHA384;
+	const uint32_t dlen = s256 ? 32 : is384 ? 48 : 64;
+	uint32_t *perm = nullptr;
+
+	if (ws != nullptr) {
+		uint32_t *hist = ws;
+		uint32_t *cursor = ws + NET2_SHA2_NBINS;
+		perm = ws + 2 * NET2_SHA2_NBINS;
+		hipError_t e = hipMemsetAsync(hist, 0,
+		    NET2_SHA2_NBINS * sizeof(uint32_t), s);
+		if (e != hipSuccess)
+			return e;
+		unsigned g = grid_for(n);
+		if (g > 2048)
+			g = 2048;
+		bin_count_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift, lenbytes,
+		    hist);
+		bin_scan_kernel<<<1, 1024, 0, s>>>(hist, cursor);
+		bin_scatter_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift,
+		    lenbytes, cursor, perm);
+	}
+	if (s256)
+		var_kernel<Sha256><<<grid_for(n), 256, 0, s>>>(base, offsets,
+		    lens, perm, n, out, dlen, 0);
+	else
+		var_kernel<Sha512><<<grid_for(n), 256, 0, s>>>(base, offsets,
+		    lens, perm, n, out, dlen, is384);
+	return hipGetLastError();
+}

@@ -1,0 +1,35 @@
+/*
+ * sha2_launch.h -- internal interface between the C-ABI shim (sha2_shim.cpp)
+ * and the kernels (sha2_kernels.hip).  Not installed; the public surface is
+ * include/net2/sha2_batch.h and include/net2/hash.h.
+ */
+#ifndef NET2_SHA2_LAUNCH_H
+#define NET2_SHA2_LAUNCH_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+/* Registry indices, shared with include/net2/hash.h. */
+#define NET2_ALG_SHA256 1
+#define NET2_ALG_SHA384 2
+#define NET2_ALG_SHA512 3
+
+/* Length bins for the variable-length path (block counts >= NBINS-1 share
+ * the last bin).  65,536-byte payloads (src/carver.c:150,161) need 1,025
+ * SHA-256 blocks, so every legal payload gets its own bin. */
+#define NET2_SHA2_NBINS 2048
+
+/* Fixed-stride batch; base/out in device memory, async on s. */
+hipError_t net2_launch_fixed(int alg, const uint8_t *base, uint64_t stride,
+    uint32_t len, uint64_t n, uint8_t *out, hipStream_t s);
+
+/*
+ * Offset/length batch.  ws == NULL hashes in submission order (no binning);
+ * otherwise ws holds 2 * NBINS + n uint32 words of scratch for the
+ * length-binned order.
+ */
+hipError_t net2_launch_var(int alg, const uint8_t *base,
+    const uint64_t *offsets, const uint32_t *lens, uint64_t n, uint8_t *out,
+    uint32_t *ws, hipStream_t s);
+
+#endif /* NET2_SHA2_LAUNCH_H */

@@ -1,0 +1,577 @@
+/*
+ * sha2_shim.cpp -- the C-ABI front of the MI355X SHA-2 path
+ * (include/net2/sha2_batch.h, include/net2/hash.h).
+ *
+ * Host orchestration only: argument checks with errno-style returns (the
+ * reference maps hash failures to ENOMEM / NET2_P{EN,DE}CODE_RESOURCE,
+ * types/signature.n2t:93-95, types/packet.n2t:246-249), device discovery,
+ * pinned staging and stream management.  Every digest is computed by the
+ * HIP kernels in sha2_kernels.hip; there is deliberately no CPU hashing
+ * path here, so a missing or unusable GPU is an ENODEV, never a silent
+ * fallback.
+ */
+#include "sha2_launch.h"
+
+#include <hip/hip_runtime.h>
+
+#include <errno.h>
+#include <stdint.h>
+#include <string.h>
+#include <sys/uio.h>
+
+#include <algorithm>
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#define NET2_EXPORT extern "C" __attribute__((visibility("default")))
+
+#include "../../include/net2/hash.h"
+
+namespace {
+
+thread_local int tl_last_hip_error = 0;
+
+int hip_fail(hipError_t e)
+{
+	tl_last_hip_error = (int)e;
+	return e == hipErrorOutOfMemory ? ENOMEM : EIO;
+}
+
+#define HIP_TRY(expr)                                                        \
+	do {                                                                 \
+		hipError_t _e = (expr);                                      \
+		if (_e != hipSuccess)                                        \
+			return hip_fail(_e);                                 \
+	} while (0)
+
+/* ---- registry (include/net2/hash.h) ------------------------------------ */
+
+struct HashRow {
+	const char *name;
+	int hashlen;
+	int keylen;
+};
+
+const HashRow kRows[] = {
+	{ "nil", 0, 0 },
+	{ "SHA256", 32, 0 },
+	{ "SHA384", 48, 0 },
+	{ "SHA512", 64, 0 },
+	{ "HMAC-SHA256", 32, 32 },
+	{ "HMAC-SHA384", 48, 48 },
+	{ "HMAC-SHA512", 64, 64 },
+};
+constexpr int kNumRows = sizeof(kRows) / sizeof(kRows[0]);
+
+bool unkeyed_sha2(int alg)
+{
+	return alg == NET2_HASH_SHA256 || alg == NET2_HASH_SHA384 ||
+	    alg == NET2_HASH_SHA512;
+}
+
+int digest_len(int alg)
+{
+	return alg >= 0 && alg < kNumRows ? kRows[alg].hashlen : -1;
+}
+
+/* ---- device discovery --------------------------------------------------- */
+
+std::once_flag g_disc_once;
+std::vector<int> g_devices;	/* HIP ordinals of usable gfx950 devices */
+
+void discover()
+{
+	int n = 0;
+	if (hipGetDeviceCount(&n) != hipSuccess)
+		return;
+	for (int d = 0; d < n; d++) {
+		hipDeviceProp_t p;
+		if (hipGetDeviceProperties(&p, d) != hipSuccess)
+			continue;
+		if (strncmp(p.gcnArchName, "gfx950", 6) == 0)
+			g_devices.push_back(d);
+	}
+}
+
+const std::vector<int> &devices()
+{
+	std::call_once(g_disc_once, discover);
+	return g_devices;
+}
+
+/* Is the calling thread's current device one we built code for? */
+int check_current_device()
+{
+	int cur = -1;
+	const std::vector<int> &dv = devices();
+	if (dv.empty())
+		return ENODEV;
+	if (hipGetDevice(&cur) != hipSuccess)
+		return ENODEV;
+	return std::find(dv.begin(), dv.end(), cur) != dv.end() ? 0 : ENODEV;
+}
+
+/* ---- per-device staging for the host-memory paths -------------------- */
+
+/*
+ * One pipeline slot: pinned input and digest staging, device input,
+ * offsets/lengths and digests, binning workspace, and a stream.  Two slots
+ * per device double-buffer host gather / H2D / kernel / D2H.
+ */
+struct Slot {
+	hipStream_t stream = nullptr;
+	hipEvent_t done = nullptr;
+	bool busy = false;
+	uint8_t *h_in = nullptr, *h_dig = nullptr;
+	uint64_t *h_off = nullptr;
+	uint32_t *h_len = nullptr;
+	uint8_t *d_in = nullptr, *d_dig = nullptr;
+	uint64_t *d_off = nullptr;
+	uint32_t *d_len = nullptr;
+	uint32_t *d_ws = nullptr;
+	size_t cap_in = 0, cap_n = 0;
+	/* digests of the chunk in flight go back to the caller here */
+	uint8_t *user_dig = nullptr;
+	size_t user_bytes = 0;
+
+	void release()
+	{
+		if (h_in) (void)hipHostFree(h_in);
+		if (h_dig) (void)hipHostFree(h_dig);
+		if (h_off) (void)hipHostFree(h_off);
+		if (h_len) (void)hipHostFree(h_len);
+		if (d_in) (void)hipFree(d_in);
+		if (d_dig) (void)hipFree(d_dig);
+		if (d_off) (void)hipFree(d_off);
+		if (d_len) (void)hipFree(d_len);
+		if (d_ws) (void)hipFree(d_ws);
+		h_in = h_dig = nullptr;
+		h_off = nullptr;
+		h_len = nullptr;
+		d_in = d_dig = nullptr;
+		d_off = nullptr;
+		d_len = d_ws = nullptr;
+		cap_in = cap_n = 0;
+	}
+
+	/* Grow to hold `in` payload bytes and `n` packets. */
+	int reserve(size_t in, size_t n)
+	{
+		if (stream == nullptr) {
+			HIP_TRY(hipStreamCreateWithFlags(&stream,
+			    hipStreamNonBlocking));
+			HIP_TRY(hipEventCreateWithFlags(&done,
+			    hipEventDisableTiming));
+		}
+		if (in <= cap_in && n <= cap_n)
+			return 0;
+		release();
+		in = std::max<size_t>(in, 4096);
+		n = std::max<size_t>(n, 64);
+		HIP_TRY(hipHostMalloc((void **)&h_in, in, hipHostMallocDefault));
+		HIP_TRY(hipHostMalloc((void **)&h_dig, n * 64,
+		    hipHostMallocDefault));
+		HIP_TRY(hipHostMalloc((void **)&h_off, n * 8,
+		    hipHostMallocDefault));
+		HIP_TRY(hipHostMalloc((void **)&h_len, n * 4,
+		    hipHostMallocDefault));
+		HIP_TRY(hipMalloc((void **)&d_in, in));
+		HIP_TRY(hipMalloc((void **)&d_dig, n * 64));
+		HIP_TRY(hipMalloc((void **)&d_off, n * 8));
+		HIP_TRY(hipMalloc((void **)&d_len, n * 4));
+		HIP_TRY(hipMalloc((void **)&d_ws,
+		    (2 * NET2_SHA2_NBINS + n) * sizeof(uint32_t)));
+		cap_in = in;
+		cap_n = n;
+		return 0;
+	}
+};
+
+struct DeviceCtx {
+	std::mutex mu;		/* one host-memory batch per device at a time */
+	Slot slot[2];
+	Slot small;		/* single-message path (hashiov, HMAC keys) */
+	std::mutex small_mu;
+};
+
+std::mutex g_ctx_mu;
+std::vector<std::unique_ptr<DeviceCtx>> g_ctx;
+
+DeviceCtx *ctx_for(size_t idx)
+{
+	std::lock_guard<std::mutex> g(g_ctx_mu);
+	if (g_ctx.size() < devices().size())
+		g_ctx.resize(devices().size());
+	if (!g_ctx[idx])
+		g_ctx[idx].reset(new DeviceCtx());
+	return g_ctx[idx].get();
+}
+
+/* Chunk payload target for the host pipeline. */
+constexpr size_t kChunkBytes = 64u << 20;
+
+/*
+ * Gather one chunk [lo, hi) of the caller's packets into slot s (packed,
+ * 16-byte aligned packet starts), enqueue H2D + kernel + D2H.
+ */
+int enqueue_chunk(Slot &s, int alg, const uint8_t *base,
+    const uint64_t *offsets, const uint32_t *lens, uint64_t stride,
+    uint32_t fixed_len, uint64_t lo, uint64_t hi, uint8_t *user_dig)
+{
+	const uint64_t n = hi - lo;
+	const int dl = digest_len(alg);
+	size_t bytes = 0;
+	int rc;
+
+	if (offsets == nullptr) {
+		bytes = (size_t)n * ((fixed_len + 15) & ~15u);
+	} else {
+		for (uint64_t i = lo; i < hi; i++)
+			bytes += ((size_t)lens[i] + 15) & ~(size_t)15;
+	}
+	if ((rc = s.reserve(bytes, n)) != 0)
+		return rc;
+
+	if (offsets == nullptr) {
+		const size_t st = (fixed_len + 15) & ~15u;
+		if (st == stride) {
+			/* contiguous; the caller's buffer ends at the last
+			 * packet's last byte, not at a stride boundary */
+			memcpy(s.h_in, base + lo * stride,
+			    (size_t)(n - 1) * stride + fixed_len);
+		} else {
+			for (uint64_t i = 0; i < n; i++)
+				memcpy(s.h_in + i * st, base + (lo + i) * stride,
+				    fixed_len);
+		}
+		HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
+		    hipMemcpyHostToDevice, s.stream));
+		HIP_TRY(net2_launch_fixed(alg, s.d_in, st, fixed_len, n,
+		    s.d_dig, s.stream));
+	} else {
+		size_t at = 0;
+		for (uint64_t i = 0; i < n; i++) {
+			const uint32_t l = lens[lo + i];
+			memcpy(s.h_in + at, base + offsets[lo + i], l);
+			s.h_off[i] = at;
+			s.h_len[i] = l;
+			at += ((size_t)l + 15) & ~(size_t)15;
+		}
+		HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
+		    hipMemcpyHostToDevice, s.stream));
+		HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, n * 8,
+		    hipMemcpyHostToDevice, s.stream));
+		HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, n * 4,
+		    hipMemcpyHostToDevice, s.stream));
+		HIP_TRY(net2_launch_var(alg, s.d_in, s.d_off, s.d_len, n,
+		    s.d_dig, n >= 4096 ? s.d_ws : nullptr, s.stream));
+	}
+	HIP_TRY(hipMemcpyAsync(s.h_dig, s.d_dig, (size_t)n * dl,
+	    hipMemcpyDeviceToHost, s.stream));
+	HIP_TRY(hipEventRecord(s.done, s.stream));
+	s.busy = true;
+	s.user_dig = user_dig;
+	s.user_bytes = (size_t)n * dl;
+	return 0;
+}
+
+int drain(Slot &s)
+{
+	if (!s.busy)
+		return 0;
+	s.busy = false;
+	HIP_TRY(hipEventSynchronize(s.done));
+	memcpy(s.user_dig, s.h_dig, s.user_bytes);
+	return 0;
+}
+
+/* One device's share of a host-memory batch. */
+int run_device_slice(size_t didx, int alg, const uint8_t *base,
+    const uint64_t *offsets, const uint32_t *lens, uint64_t stride,
+    uint32_t fixed_len, uint64_t lo, uint64_t hi, uint8_t *digests)
+{
+	DeviceCtx *c = ctx_for(didx);
+	std::lock_guard<std::mutex> g(c->mu);
+	const int dl = digest_len(alg);
+	int rc = 0, cur = 0;
+
+	HIP_TRY(hipSetDevice(devices()[didx]));
+	for (uint64_t at = lo; at < hi && rc == 0;) {
+		/* chunk end: at most kChunkBytes of (padded) payload */
+		uint64_t end = at;
+		size_t bytes = 0;
+		if (offsets == nullptr) {
+			const size_t per = std::max<size_t>(
+			    (fixed_len + 15) & ~15u, 16);
+			end = std::min<uint64_t>(hi, at + std::max<size_t>(
+			    kChunkBytes / per, 1));
+		} else {
+			while (end < hi && (bytes == 0 ||
+			    bytes + lens[end] <= kChunkBytes)) {
+				bytes += ((size_t)lens[end] + 15) & ~(size_t)15;
+				end++;
+			}
+		}
+		Slot &s = c->slot[cur];
+		if ((rc = drain(s)) != 0)
+			break;
+		rc = enqueue_chunk(s, alg, base, offsets, lens, stride,
+		    fixed_len, at, end, digests + at * dl);
+		at = end;
+		cur ^= 1;
+	}
+	int rc2 = drain(c->slot[0]);
+	int rc3 = drain(c->slot[1]);
+	return rc ? rc : rc2 ? rc2 : rc3;
+}
+
+/* Single message, gathered from iovecs, on the first device. */
+int hash_small(int alg, const struct iovec *iov, size_t iovcnt, uint8_t *out)
+{
+	size_t total = 0;
+	for (size_t i = 0; i < iovcnt; i++)
+		total += iov[i].iov_len;
+	if (total > UINT32_MAX)
+		return EINVAL;
+	DeviceCtx *c = ctx_for(0);
+	std::lock_guard<std::mutex> g(c->small_mu);
+	int prev = -1;
+	(void)hipGetDevice(&prev);
+	HIP_TRY(hipSetDevice(devices()[0]));
+	Slot &s = c->small;
+	int rc = s.reserve(total, 1);
+	if (rc != 0)
+		return rc;
+	size_t at = 0;
+	for (size_t i = 0; i < iovcnt; i++) {
+		if (iov[i].iov_len)
+			memcpy(s.h_in + at, iov[i].iov_base, iov[i].iov_len);
+		at += iov[i].iov_len;
+	}
+	const int dl = digest_len(alg);
+	HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, std::max<size_t>(total, 1),
+	    hipMemcpyHostToDevice, s.stream));
+	HIP_TRY(net2_launch_fixed(alg, s.d_in, std::max<size_t>(total, 16),
+	    (uint32_t)total, 1, s.d_dig, s.stream));
+	HIP_TRY(hipMemcpyAsync(s.h_dig, s.d_dig, dl, hipMemcpyDeviceToHost,
+	    s.stream));
+	HIP_TRY(hipStreamSynchronize(s.stream));
+	memcpy(out, s.h_dig, dl);
+	if (prev >= 0)
+		(void)hipSetDevice(prev);
+	return 0;
+}
+
+} /* namespace */
+
+/* ---- exported C ABI ---------------------------------------------------- */
+
+NET2_EXPORT const int net2_hashmax = kNumRows;
+
+NET2_EXPORT int net2_sha2_abi_version(void)
+{
+	return NET2_SHA2_ABI_VERSION;
+}
+
+NET2_EXPORT int net2_sha2_device_count(int *count)
+{
+	if (count == nullptr)
+		return EINVAL;
+	*count = (int)devices().size();
+	return *count > 0 ? 0 : ENODEV;
+}
+
+NET2_EXPORT int net2_sha2_last_hip_error(void)
+{
+	return tl_last_hip_error;
+}
+
+NET2_EXPORT const char *net2_sha2_strerror(int err)
+{
+	switch (err) {
+	case 0: return "success";
+	case EINVAL: return "invalid argument";
+	case ENOMEM: return "out of memory";
+	case ENODEV: return "no usable gfx950 (MI355X) device";
+	case EIO: return "HIP runtime error";
+	case ENOSYS: return "not implemented";
+	default: return "unknown error";
+	}
+}
+
+NET2_EXPORT int net2_sha2_dev_fixed(int alg, const void *d_base,
+    uint64_t stride, uint32_t len, uint64_t n, void *d_digests, void *stream)
+{
+	if (!unkeyed_sha2(alg))
+		return EINVAL;
+	if (n == 0)
+		return 0;
+	if (d_digests == nullptr || (d_base == nullptr && len > 0))
+		return EINVAL;
+	if (n > 1 && stride < len)
+		return EINVAL;
+	int rc = check_current_device();
+	if (rc != 0)
+		return rc;
+	HIP_TRY(net2_launch_fixed(alg, (const uint8_t *)d_base, stride, len, n,
+	    (uint8_t *)d_digests, (hipStream_t)stream));
+	return 0;
+}
+
+NET2_EXPORT size_t net2_sha2_dev_var_workspace(uint64_t n)
+{
+	return (2 * (size_t)NET2_SHA2_NBINS + (size_t)n) * sizeof(uint32_t);
+}
+
+NET2_EXPORT int net2_sha2_dev_var(int alg, const void *d_base,
+    const uint64_t *d_offsets, const uint32_t *d_lens, uint64_t n,
+    void *d_digests, void *d_ws, size_t ws_bytes, void *stream)
+{
+	if (!unkeyed_sha2(alg))
+		return EINVAL;
+	if (n == 0)
+		return 0;
+	if (d_offsets == nullptr || d_lens == nullptr || d_digests == nullptr)
+		return EINVAL;
+	if (d_ws != nullptr && (ws_bytes < net2_sha2_dev_var_workspace(n) ||
+	    ((uintptr_t)d_ws & 3) != 0 || n > UINT32_MAX))
+		return EINVAL;
+	int rc = check_current_device();
+	if (rc != 0)
+		return rc;
+	HIP_TRY(net2_launch_var(alg, (const uint8_t *)d_base, d_offsets, d_lens,
+	    n, (uint8_t *)d_digests, (uint32_t *)d_ws, (hipStream_t)stream));
+	return 0;
+}
+
+NET2_EXPORT int net2_sha2_batch(int alg, const void *base,
+    const uint64_t *offsets, const uint32_t *lens, uint64_t stride,
+    uint32_t fixed_len, uint64_t n, void *digests, int max_devices)
+{
+	if (!unkeyed_sha2(alg))
+		return EINVAL;
+	if (n == 0)
+		return 0;
+	if (digests == nullptr || (offsets != nullptr && lens == nullptr))
+		return EINVAL;
+	if (offsets == nullptr && (base == nullptr && fixed_len > 0))
+		return EINVAL;
+	if (offsets == nullptr && n > 1 && stride < fixed_len)
+		return EINVAL;
+	const std::vector<int> &dv = devices();
+	if (dv.empty())
+		return ENODEV;
+	size_t nd = dv.size();
+	if (max_devices > 0 && (size_t)max_devices < nd)
+		nd = (size_t)max_devices;
+	if ((uint64_t)nd > n)
+		nd = (size_t)n;
+
+	/* Contiguous slices: by packet count, or by bytes for var layout. */
+	std::vector<uint64_t> cut(nd + 1, 0);
+	cut[nd] = n;
+	if (offsets == nullptr) {
+		for (size_t d = 1; d < nd; d++)
+			cut[d] = n * d / nd;
+	} else {
+		uint64_t total = 0, acc = 0;
+		for (uint64_t i = 0; i < n; i++)
+			total += lens[i];
+		size_t d = 1;
+		for (uint64_t i = 0; i < n && d < nd; i++) {
+			acc += lens[i];
+			while (d < nd && acc * nd >= total * d)
+				cut[d++] = i + 1;
+		}
+		for (; d < nd; d++)
+			cut[d] = n;
+	}
+
+	/* Device list starts at the caller's current device, so one process
+	 * per GPU with max_devices == 1 stays on its own device. */
+	int prev = -1;
+	(void)hipGetDevice(&prev);
+	size_t first = 0;
+	for (size_t d = 0; d < dv.size(); d++)
+		if (dv[d] == prev)
+			first = d;
+	std::vector<int> rcs(nd, 0);
+	std::vector<std::thread> th;
+	for (size_t d = 1; d < nd; d++)
+		th.emplace_back([&, d]() {
+			rcs[d] = run_device_slice((first + d) % dv.size(), alg,
+			    (const uint8_t *)base, offsets, lens, stride,
+			    fixed_len, cut[d], cut[d + 1], (uint8_t *)digests);
+		});
+	rcs[0] = run_device_slice(first, alg, (const uint8_t *)base, offsets,
+	    lens, stride, fixed_len, cut[0], cut[1], (uint8_t *)digests);
+	for (std::thread &t : th)
+		t.join();
+	if (prev >= 0)
+		(void)hipSetDevice(prev);
+	for (int r : rcs)
+		if (r != 0)
+			return r;
+	return 0;
+}
+
+NET2_EXPORT const char *net2_hash_getname(int alg)
+{
+	return alg >= 0 && alg < kNumRows ? kRows[alg].name : nullptr;
+}
+
+NET2_EXPORT int net2_hash_findname(const char *name)
+{
+	if (name == nullptr)
+		return -1;
+	for (int i = 0; i < kNumRows; i++)
+		if (strcmp(kRows[i].name, name) == 0)
+			return i;
+	return -1;
+}
+
+NET2_EXPORT int net2_hash_gethashlen(int alg)
+{
+	return alg >= 0 && alg < kNumRows ? kRows[alg].hashlen : -1;
+}
+
+NET2_EXPORT int net2_hash_getkeylen(int alg)
+{
+	return alg >= 0 && alg < kNumRows ? kRows[alg].keylen : -1;
+}
+
+NET2_EXPORT int net2_hashctx_hashiov(int alg, const void *key, size_t keylen,
+    const struct iovec *iov, size_t iovcnt, void *out, size_t outlen)
+{
+	if (alg < 0 || alg >= kNumRows)
+		return EINVAL;
+	if ((size_t)kRows[alg].keylen != keylen ||
+	    (keylen > 0 && key == nullptr))
+		return EINVAL;
+	if (iovcnt > 0 && iov == nullptr)
+		return EINVAL;
+	if (alg == NET2_HASH_NIL)
+		return 0;
+	if (out == nullptr || outlen < (size_t)kRows[alg].hashlen)
+		return EINVAL;
+	if (devices().empty())
+		return ENODEV;
+	if (!unkeyed_sha2(alg))
+		return ENOSYS;	/* keyed rows: see net2_hmac_dev */
+	return hash_small(alg, iov, iovcnt, (uint8_t *)out);
+}
+
+NET2_EXPORT int net2_hmac_dev(int alg, const void *key, size_t keylen,
+    const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
+    uint64_t stride, uint32_t fixed_len, uint64_t n, void *d_digests,
+    void *stream)
+{
+	(void)key; (void)keylen; (void)d_base; (void)d_offsets; (void)d_lens;
+	(void)stride; (void)fixed_len; (void)n; (void)d_digests; (void)stream;
+	if (alg < NET2_HASH_HMAC_SHA256 || alg > NET2_HASH_HMAC_SHA512)
+		return EINVAL;
+	return ENOSYS;
+}

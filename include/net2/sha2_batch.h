@@ -1,0 +1,107 @@
+/*
+ * net2/sha2_batch.h -- C ABI of the MI355X batched SHA-2 digest path.
+ *
+ * Drop-in boundary for the reference's SHA-2 integrity hash:
+ *   - replaces the per-payload SHA{256,384,512}Init/Update/Final sequence of
+ *     src/sha2.c:280-563 / :566-919 (declared in the absent
+ *     include/ilias/net2/bsd_compat/sha2.h, included from src/sha2.c:38,
+ *     src/sign.c:36, types/packet.n2t:80) with one call over many
+ *     independent packets;
+ *   - is what net2_hashctx_hashbuf (called at types/signature.n2t:92,147)
+ *     and net2_signctx_fingerprint (src/sign.c:298-307) bottom out in; see
+ *     net2/hash.h for that registry layer.
+ *
+ * Conventions:
+ *   - plain pointers and sizes only; no HIP, torch or C++ types;
+ *   - return 0 on success, or an errno value: EINVAL (bad alg / argument),
+ *     ENOMEM (allocation), ENODEV (no usable MI355X), EIO (HIP runtime
+ *     error; net2_sha2_last_hip_error() has the HIP code).  Nothing aborts;
+ *   - thread-safe: calls may come from any number of host threads (the
+ *     reference runs signature work on threadpool workers,
+ *     include/ilias/net2/threadpool.h:33-34);
+ *   - there is no CPU fallback: without a usable gfx950 device every
+ *     compute entry point fails with ENODEV.
+ *
+ * Digest byte order and values are those of src/sha2.c's *Final
+ * (big-endian state words, 32 / 48 / 64 bytes).
+ */
+#ifndef NET2_SHA2_BATCH_H
+#define NET2_SHA2_BATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NET2_SHA2_ABI_VERSION 1
+
+/* Algorithm indices = rows of the hash registry in net2/hash.h. */
+#define NET2_HASH_NIL		0
+#define NET2_HASH_SHA256	1
+#define NET2_HASH_SHA384	2
+#define NET2_HASH_SHA512	3
+#define NET2_HASH_HMAC_SHA256	4
+#define NET2_HASH_HMAC_SHA384	5
+#define NET2_HASH_HMAC_SHA512	6
+
+/* ABI version of the loaded library (NET2_SHA2_ABI_VERSION). */
+int net2_sha2_abi_version(void);
+
+/* Number of usable gfx950 devices, via *count.  0 / ENODEV. */
+int net2_sha2_device_count(int *count);
+
+/* HIP error code behind the calling thread's last EIO (0 if none). */
+int net2_sha2_last_hip_error(void);
+
+/* Human-readable text for a return code of this API. */
+const char *net2_sha2_strerror(int err);
+
+/*
+ * Device-resident batch, fixed stride (config "1M x 1 KiB").
+ * Packet i is d_base[i * stride .. i * stride + len); its digest is written
+ * to d_digests + i * hashlen (32 / 48 / 64).  All pointers are device
+ * memory of the calling thread's current HIP device.  Asynchronous on
+ * `stream` (a hipStream_t; NULL = the null stream); the call returns once
+ * the work is enqueued.  Requires len <= stride when n > 1.
+ */
+int net2_sha2_dev_fixed(int alg, const void *d_base, uint64_t stride,
+    uint32_t len, uint64_t n, void *d_digests, void *stream);
+
+/*
+ * Device-resident batch, packed variable-length packets (config "1M x
+ * mixed {64, 512, 1500} B"): packet i is d_base[d_offsets[i] ..
+ * d_offsets[i] + d_lens[i]).  Lengths are binned on the device so lanes of
+ * a wave share a block count; d_ws must hold
+ * net2_sha2_dev_var_workspace(n) bytes of device memory (4-byte aligned)
+ * or be NULL to hash in submission order (slower on mixed lengths).
+ * Asynchronous on `stream`; d_ws must stay allocated until it completes.
+ */
+int net2_sha2_dev_var(int alg, const void *d_base, const uint64_t *d_offsets,
+    const uint32_t *d_lens, uint64_t n, void *d_digests, void *d_ws,
+    size_t ws_bytes, void *stream);
+
+/* Bytes of scratch net2_sha2_dev_var needs for n packets. */
+size_t net2_sha2_dev_var_workspace(uint64_t n);
+
+/*
+ * Host-memory batch, end to end: packets are read from host memory,
+ * staged through pinned buffers to every usable device (contiguous packet
+ * slices, one host thread and stream pair per device, H2D / kernel / D2H
+ * double-buffered), and the digests written back to host memory.
+ * Synchronous.  offsets == NULL selects the fixed layout
+ * base[i * stride .. + fixed_len); otherwise packet i is
+ * base[offsets[i] .. + lens[i]) and stride / fixed_len are ignored.
+ * max_devices <= 0 uses every device; the device list starts at the
+ * calling thread's current HIP device (so max_devices == 1 means "this
+ * device" for a one-process-per-GPU caller).
+ */
+int net2_sha2_batch(int alg, const void *base, const uint64_t *offsets,
+    const uint32_t *lens, uint64_t stride, uint32_t fixed_len, uint64_t n,
+    void *digests, int max_devices);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NET2_SHA2_BATCH_H */

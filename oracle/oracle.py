@@ -1,0 +1,97 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes binding of the CPU oracle.
+
+Loads oracle/liboracle_sha2.so (built from oracle/sha2_oracle.c by
+oracle/Makefile), the clean-room restatement of the reference's src/sha2.c.
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it,
+always as the checker / CPU baseline, never as the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle_sha2.so")
+
+DIGEST_LEN = {1: 32, 2: 48, 3: 64, 4: 32, 5: 48, 6: 64}
+
+
+class Ctx(ctypes.Structure):
+    """oracle_sha2_ctx == the reference SHA2_CTX layout (208 bytes)."""
+    _fields_ = [("st", ctypes.c_uint64 * 8), ("bits", ctypes.c_uint64 * 2),
+                ("blk", ctypes.c_uint8 * 128)]
+
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        L.oracle_sha2_digest.argtypes = [ctypes.c_int, vp, sz, vp]
+        L.oracle_sha2_digest.restype = ctypes.c_int
+        L.oracle_hmac_digest.argtypes = [ctypes.c_int, vp, sz, vp, sz, vp]
+        L.oracle_hmac_digest.restype = ctypes.c_int
+        L.oracle_sha2_batch.argtypes = [ctypes.c_int, vp, vp, vp,
+                                        ctypes.c_uint64, ctypes.c_uint32, sz,
+                                        vp, ctypes.c_int]
+        L.oracle_sha2_batch.restype = ctypes.c_int
+        for pfx in ("sha256", "sha384", "sha512"):
+            for fn, args in (("init", [vp]), ("update", [vp, vp, sz]),
+                             ("pad", [vp]), ("final", [vp, vp])):
+                f = getattr(L, f"oracle_{pfx}_{fn}")
+                f.argtypes = args
+                f.restype = None
+        _lib = L
+    return _lib
+
+
+def digest(alg: int, msg: bytes) -> bytes:
+    out = ctypes.create_string_buffer(64)
+    buf = ctypes.create_string_buffer(bytes(msg), max(len(msg), 1))
+    n = lib().oracle_sha2_digest(alg, buf, len(msg), out)
+    if n < 0:
+        raise ValueError(f"bad alg {alg}")
+    return out.raw[:n]
+
+
+def hmac(alg: int, key: bytes, msg: bytes) -> bytes:
+    out = ctypes.create_string_buffer(64)
+    kb = ctypes.create_string_buffer(bytes(key), max(len(key), 1))
+    mb = ctypes.create_string_buffer(bytes(msg), max(len(msg), 1))
+    n = lib().oracle_hmac_digest(alg, kb, len(key), mb, len(msg), out)
+    if n < 0:
+        raise ValueError(f"bad alg {alg}")
+    return out.raw[:n]
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def batch(alg: int, data: np.ndarray, offsets=None, lens=None, stride=0,
+          length=0, n=None, nthreads=1) -> np.ndarray:
+    """CPU digests of a packet batch, same layouts as net2_sha2_batch."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    if offsets is not None:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        n = len(offsets)
+    out = np.empty((n, DIGEST_LEN[alg]), dtype=np.uint8)
+    rc = lib().oracle_sha2_batch(alg, _ptr(data), _ptr(offsets), _ptr(lens),
+                                 stride, length, n, _ptr(out), nthreads)
+    if rc != 0:
+        raise ValueError(f"bad alg {alg}")
+    return out

@@ -1,0 +1,495 @@
+/*
+ * sha2_oracle.c -- TEST INFRASTRUCTURE ONLY (see sha2_oracle.h).
+ *
+ * A clean-room restatement of FIPS 180-4 SHA-256/384/512 that reproduces the
+ * call semantics of the reference's src/sha2.c:
+ *   - Init on a NULL context is a no-op            (src/sha2.c:283, 569, 867)
+ *   - Update with len == 0 is a no-op              (src/sha2.c:455, 744)
+ *   - Update transforms whole blocks straight from caller memory and buffers
+ *     the remainder                                (src/sha2.c:461-492, 750-781)
+ *   - Pad appends 0x80, zero-fills and stores the bit length big-endian; a
+ *     second block is needed when the tail leaves < 8 (SHA-256) or < 16
+ *     (SHA-384/512) free bytes                     (src/sha2.c:495-543, 784-832)
+ *   - Final(NULL, ctx) leaves the context untouched for SHA-256/512
+ *     (src/sha2.c:551-562, 840-858) while SHA-384 zeroes it regardless
+ *     (src/sha2.c:918).
+ * The compression functions follow the rolled transforms of
+ * src/sha2.c:374-445 (SHA-256) and :663-734 (SHA-512); the round constants
+ * and initial values are the FIPS 180-4 tables that src/sha2.c:178-276 holds.
+ */
+#include "sha2_oracle.h"
+
+#include <pthread.h>
+#include <string.h>
+
+/* ---- FIPS 180-4 section 4.2.2 / 4.2.3 constants -------------------- */
+
+static const uint32_t k32[64] = {
+	0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1,
+	0x923f82a4, 0xab1c5ed5, 0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3,
+	0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786,
+	0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+	0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147,
+	0x06ca6351, 0x14292967, 0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13,
+	0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85, 0xa2bfe8a1, 0xa81a664b,
+	0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+	0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a,
+	0x5b9cca4f, 0x682e6ff3, 0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208,
+	0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2,
+};
+
+static const uint64_t k64[80] = {
+	0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL,
+	0xe9b5dba58189dbbcULL, 0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL,
+	0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL, 0xd807aa98a3030242ULL,
+	0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+	0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL,
+	0xc19bf174cf692694ULL, 0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL,
+	0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL, 0x2de92c6f592b0275ULL,
+	0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+	0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL,
+	0xbf597fc7beef0ee4ULL, 0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL,
+	0x06ca6351e003826fULL, 0x142929670a0e6e70ULL, 0x27b70a8546d22ffcULL,
+	0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+	0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL,
+	0x92722c851482353bULL, 0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL,
+	0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL, 0xd192e819d6ef5218ULL,
+	0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+	0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL,
+	0x34b0bcb5e19b48a8ULL, 0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL,
+	0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL, 0x748f82ee5defb2fcULL,
+	0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+	0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL,
+	0xc67178f2e372532bULL, 0xca273eceea26619cULL, 0xd186b8c721c0c207ULL,
+	0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL, 0x06f067aa72176fbaULL,
+	0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+	0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL,
+	0x431d67c49c100d4cULL, 0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL,
+	0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL,
+};
+
+static const uint32_t iv256[8] = {
+	0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+	0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19,
+};
+
+static const uint64_t iv384[8] = {
+	0xcbbb9d5dc1059ed8ULL, 0x629a292a367cd507ULL, 0x9159015a3070dd17ULL,
+	0x152fecd8f70e5939ULL, 0x67332667ffc00b31ULL, 0x8eb44a8768581511ULL,
+	0xdb0c2e0d64f98fa7ULL, 0x47b5481dbefa4fa4ULL,
+};
+
+static const uint64_t iv512[8] = {
+	0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+	0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+	0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL,
+};
+
+/* ---- byte order helpers ------------------------------------------------ */
+
+static inline uint32_t load_be32(const uint8_t *p)
+{
+	return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) |
+	    ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+
+static inline uint64_t load_be64(const uint8_t *p)
+{
+	return ((uint64_t)load_be32(p) << 32) | load_be32(p + 4);
+}
+
+static inline void store_be32(uint8_t *p, uint32_t v)
+{
+	for (int i = 3; i >= 0; i--, v >>= 8)
+		p[i] = (uint8_t)v;
+}
+
+static inline void store_be64(uint8_t *p, uint64_t v)
+{
+	store_be32(p, (uint32_t)(v >> 32));
+	store_be32(p + 4, (uint32_t)v);
+}
+
+static inline uint32_t ror32(uint32_t x, unsigned n)
+{
+	return (x >> n) | (x << (32 - n));
+}
+
+static inline uint64_t ror64(uint64_t x, unsigned n)
+{
+	return (x >> n) | (x << (64 - n));
+}
+
+/* ---- compression functions (FIPS 180-4 6.2.2 / 6.4.2) ------------------ */
+
+void oracle_sha256_transform(uint32_t st[8], const uint8_t blk[64])
+{
+	uint32_t w[64], v[8];
+	int t;
+
+	for (t = 0; t < 16; t++)
+		w[t] = load_be32(blk + 4 * t);
+	for (t = 16; t < 64; t++) {
+		uint32_t s0 = ror32(w[t - 15], 7) ^ ror32(w[t - 15], 18) ^
+		    (w[t - 15] >> 3);
+		uint32_t s1 = ror32(w[t - 2], 17) ^ ror32(w[t - 2], 19) ^
+		    (w[t - 2] >> 10);
+		w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+	}
+	memcpy(v, st, sizeof(v));
+	for (t = 0; t < 64; t++) {
+		/* v[0..7] = a..h */
+		uint32_t e = v[4], a = v[0];
+		uint32_t big1 = ror32(e, 6) ^ ror32(e, 11) ^ ror32(e, 25);
+		uint32_t ch = (e & v[5]) ^ (~e & v[6]);
+		uint32_t t1 = v[7] + big1 + ch + k32[t] + w[t];
+		uint32_t big0 = ror32(a, 2) ^ ror32(a, 13) ^ ror32(a, 22);
+		uint32_t maj = (a & v[1]) ^ (a & v[2]) ^ (v[1] & v[2]);
+		memmove(v + 1, v, 7 * sizeof(v[0]));
+		v[4] += t1;
+		v[0] = t1 + big0 + maj;
+	}
+	for (t = 0; t < 8; t++)
+		st[t] += v[t];
+}
+
+void oracle_sha512_transform(uint64_t st[8], const uint8_t blk[128])
+{
+	uint64_t w[80], v[8];
+	int t;
+
+	for (t = 0; t < 16; t++)
+		w[t] = load_be64(blk + 8 * t);
+	for (t = 16; t < 80; t++) {
+		uint64_t s0 = ror64(w[t - 15], 1) ^ ror64(w[t - 15], 8) ^
+		    (w[t - 15] >> 7);
+		uint64_t s1 = ror64(w[t - 2], 19) ^ ror64(w[t - 2], 61) ^
+		    (w[t - 2] >> 6);
+		w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+	}
+	memcpy(v, st, sizeof(v));
+	for (t = 0; t < 80; t++) {
+		uint64_t e = v[4], a = v[0];
+		uint64_t big1 = ror64(e, 14) ^ ror64(e, 18) ^ ror64(e, 41);
+		uint64_t ch = (e & v[5]) ^ (~e & v[6]);
+		uint64_t t1 = v[7] + big1 + ch + k64[t] + w[t];
+		uint64_t big0 = ror64(a, 28) ^ ror64(a, 34) ^ ror64(a, 39);
+		uint64_t maj = (a & v[1]) ^ (a & v[2]) ^ (v[1] & v[2]);
+		memmove(v + 1, v, 7 * sizeof(v[0]));
+		v[4] += t1;
+		v[0] = t1 + big0 + maj;
+	}
+	for (t = 0; t < 8; t++)
+		st[t] += v[t];
+}
+
+/* ---- SHA-256 streaming API ---------------------------------------------- */
+
+void oracle_sha256_init(oracle_sha2_ctx *c)
+{
+	if (c == NULL)
+		return;
+	memcpy(c->st.w32, iv256, sizeof(iv256));
+	memset(c->blk, 0, sizeof(c->blk));
+	c->bits[0] = 0;
+}
+
+void oracle_sha256_update(oracle_sha2_ctx *c, const uint8_t *p, size_t len)
+{
+	size_t have, take;
+
+	if (len == 0)
+		return;
+	have = (size_t)((c->bits[0] >> 3) & (ORACLE_SHA256_BLOCK - 1));
+	if (have != 0) {
+		take = ORACLE_SHA256_BLOCK - have;
+		if (take > len)
+			take = len;
+		memcpy(c->blk + have, p, take);
+		c->bits[0] += (uint64_t)take << 3;
+		p += take;
+		len -= take;
+		if (have + take < ORACLE_SHA256_BLOCK)
+			return;
+		oracle_sha256_transform(c->st.w32, c->blk);
+	}
+	for (; len >= ORACLE_SHA256_BLOCK; len -= ORACLE_SHA256_BLOCK,
+	    p += ORACLE_SHA256_BLOCK) {
+		oracle_sha256_transform(c->st.w32, p);
+		c->bits[0] += ORACLE_SHA256_BLOCK << 3;
+	}
+	if (len != 0) {
+		memcpy(c->blk, p, len);
+		c->bits[0] += (uint64_t)len << 3;
+	}
+}
+
+void oracle_sha256_pad(oracle_sha2_ctx *c)
+{
+	size_t have = (size_t)((c->bits[0] >> 3) & (ORACLE_SHA256_BLOCK - 1));
+
+	c->blk[have++] = 0x80;
+	if (have > ORACLE_SHA256_BLOCK - 8) {
+		/* No room for the 8-byte length: flush one more block. */
+		memset(c->blk + have, 0, ORACLE_SHA256_BLOCK - have);
+		oracle_sha256_transform(c->st.w32, c->blk);
+		have = 0;
+	}
+	memset(c->blk + have, 0, ORACLE_SHA256_BLOCK - 8 - have);
+	store_be64(c->blk + ORACLE_SHA256_BLOCK - 8, c->bits[0]);
+	oracle_sha256_transform(c->st.w32, c->blk);
+}
+
+void oracle_sha256_final(uint8_t *digest, oracle_sha2_ctx *c)
+{
+	oracle_sha256_pad(c);
+	if (digest == NULL)
+		return;
+	for (int i = 0; i < 8; i++)
+		store_be32(digest + 4 * i, c->st.w32[i]);
+	memset(c, 0, sizeof(*c));
+}
+
+/* ---- SHA-512 / SHA-384 streaming API ---------------------------------- */
+
+static void sha512_init_from(oracle_sha2_ctx *c, const uint64_t iv[8])
+{
+	if (c == NULL)
+		return;
+	memcpy(c->st.w64, iv, 8 * sizeof(uint64_t));
+	memset(c->blk, 0, sizeof(c->blk));
+	c->bits[0] = c->bits[1] = 0;
+}
+
+void oracle_sha512_init(oracle_sha2_ctx *c) { sha512_init_from(c, iv512); }
+void oracle_sha384_init(oracle_sha2_ctx *c) { sha512_init_from(c, iv384); }
+
+/* 128-bit bit counter += n bits (the carry src/sha2.c:136-141 propagates) */
+static inline void add_bits128(uint64_t bits[2], uint64_t n)
+{
+	bits[0] += n;
+	if (bits[0] < n)
+		bits[1]++;
+}
+
+void oracle_sha512_update(oracle_sha2_ctx *c, const uint8_t *p, size_t len)
+{
+	size_t have, take;
+
+	if (len == 0)
+		return;
+	have = (size_t)((c->bits[0] >> 3) & (ORACLE_SHA512_BLOCK - 1));
+	if (have != 0) {
+		take = ORACLE_SHA512_BLOCK - have;
+		if (take > len)
+			take = len;
+		memcpy(c->blk + have, p, take);
+		add_bits128(c->bits, (uint64_t)take << 3);
+		p += take;
+		len -= take;
+		if (have + take < ORACLE_SHA512_BLOCK)
+			return;
+		oracle_sha512_transform(c->st.w64, c->blk);
+	}
+	for (; len >= ORACLE_SHA512_BLOCK; len -= ORACLE_SHA512_BLOCK,
+	    p += ORACLE_SHA512_BLOCK) {
+		oracle_sha512_transform(c->st.w64, p);
+		add_bits128(c->bits, ORACLE_SHA512_BLOCK << 3);
+	}
+	if (len != 0) {
+		memcpy(c->blk, p, len);
+		add_bits128(c->bits, (uint64_t)len << 3);
+	}
+}
+
+void oracle_sha384_update(oracle_sha2_ctx *c, const uint8_t *p, size_t len)
+{
+	oracle_sha512_update(c, p, len);
+}
+
+void oracle_sha512_pad(oracle_sha2_ctx *c)
+{
+	size_t have = (size_t)((c->bits[0] >> 3) & (ORACLE_SHA512_BLOCK - 1));
+
+	c->blk[have++] = 0x80;
+	if (have > ORACLE_SHA512_BLOCK - 16) {
+		memset(c->blk + have, 0, ORACLE_SHA512_BLOCK - have);
+		oracle_sha512_transform(c->st.w64, c->blk);
+		have = 0;
+	}
+	memset(c->blk + have, 0, ORACLE_SHA512_BLOCK - 16 - have);
+	store_be64(c->blk + ORACLE_SHA512_BLOCK - 16, c->bits[1]);
+	store_be64(c->blk + ORACLE_SHA512_BLOCK - 8, c->bits[0]);
+	oracle_sha512_transform(c->st.w64, c->blk);
+}
+
+void oracle_sha384_pad(oracle_sha2_ctx *c) { oracle_sha512_pad(c); }
+
+void oracle_sha512_final(uint8_t *digest, oracle_sha2_ctx *c)
+{
+	oracle_sha512_pad(c);
+	if (digest == NULL)
+		return;
+	for (int i = 0; i < 8; i++)
+		store_be64(digest + 8 * i, c->st.w64[i]);
+	memset(c, 0, sizeof(*c));
+}
+
+void oracle_sha384_final(uint8_t *digest, oracle_sha2_ctx *c)
+{
+	oracle_sha512_pad(c);
+	if (digest != NULL)
+		for (int i = 0; i < 6; i++)
+			store_be64(digest + 8 * i, c->st.w64[i]);
+	memset(c, 0, sizeof(*c));	/* unconditional, src/sha2.c:918 */
+}
+
+/* ---- one-shot and batched -------------------------------------------- */
+
+int oracle_sha2_digest(int alg, const uint8_t *msg, size_t len, uint8_t *out)
+{
+	oracle_sha2_ctx c;
+
+	switch (alg) {
+	case 1:
+		oracle_sha256_init(&c);
+		oracle_sha256_update(&c, msg, len);
+		oracle_sha256_final(out, &c);
+		return ORACLE_SHA256_DIGEST;
+	case 2:
+		oracle_sha384_init(&c);
+		oracle_sha384_update(&c, msg, len);
+		oracle_sha384_final(out, &c);
+		return ORACLE_SHA384_DIGEST;
+	case 3:
+		oracle_sha512_init(&c);
+		oracle_sha512_update(&c, msg, len);
+		oracle_sha512_final(out, &c);
+		return ORACLE_SHA512_DIGEST;
+	default:
+		return -1;
+	}
+}
+
+struct batch_slice {
+	int alg, dlen;
+	const uint8_t *base;
+	const uint64_t *offsets;
+	const uint32_t *lens;
+	uint64_t stride;
+	uint32_t fixed_len;
+	size_t lo, hi;
+	uint8_t *out;
+};
+
+static void *batch_worker(void *arg)
+{
+	struct batch_slice *s = arg;
+
+	for (size_t i = s->lo; i < s->hi; i++) {
+		const uint8_t *m;
+		size_t len;
+
+		if (s->offsets != NULL) {
+			m = s->base + s->offsets[i];
+			len = s->lens[i];
+		} else {
+			m = s->base + (uint64_t)i * s->stride;
+			len = s->fixed_len;
+		}
+		oracle_sha2_digest(s->alg, m, len, s->out + i * s->dlen);
+	}
+	return NULL;
+}
+
+int oracle_sha2_batch(int alg, const uint8_t *base, const uint64_t *offsets,
+    const uint32_t *lens, uint64_t stride, uint32_t fixed_len, size_t n,
+    uint8_t *out, int nthreads)
+{
+	static const int dlen_of[4] = { 0, 32, 48, 64 };
+	struct batch_slice sl[256];
+	pthread_t tid[256];
+	int t, started;
+
+	if (alg < 1 || alg > 3)
+		return -1;
+	if (nthreads < 1)
+		nthreads = 1;
+	if (nthreads > 256)
+		nthreads = 256;
+	if ((size_t)nthreads > n)
+		nthreads = n > 0 ? (int)n : 1;
+	for (t = 0; t < nthreads; t++) {
+		sl[t] = (struct batch_slice){ alg, dlen_of[alg], base, offsets,
+		    lens, stride, fixed_len, n * t / nthreads,
+		    n * (t + 1) / nthreads, out };
+	}
+	if (nthreads == 1) {
+		batch_worker(&sl[0]);
+		return 0;
+	}
+	for (started = 0; started < nthreads; started++)
+		if (pthread_create(&tid[started], NULL, batch_worker,
+		    &sl[started]) != 0)
+			break;
+	for (t = started; t < nthreads; t++)	/* could not spawn: run inline */
+		batch_worker(&sl[t]);
+	for (t = 0; t < started; t++)
+		pthread_join(tid[t], NULL);
+	return 0;
+}
+
+/* ---- HMAC (RFC 2104 / FIPS 198-1) --------------------------------------- */
+
+int oracle_hmac_digest(int alg, const uint8_t *key, size_t keylen,
+    const uint8_t *msg, size_t len, uint8_t *out)
+{
+	int halg = alg - 3;	/* HMAC-SHA256/384/512 -> SHA-256/384/512 */
+	size_t bsz, dlen;
+	uint8_t k0[128], pad[128], inner[64];
+	oracle_sha2_ctx c;
+
+	if (halg < 1 || halg > 3)
+		return -1;
+	bsz = halg == 1 ? 64 : 128;
+	dlen = halg == 1 ? 32 : halg == 2 ? 48 : 64;
+	memset(k0, 0, sizeof(k0));
+	if (keylen > bsz)
+		oracle_sha2_digest(halg, key, keylen, k0);
+	else if (keylen > 0)
+		memcpy(k0, key, keylen);
+
+	for (size_t i = 0; i < bsz; i++)
+		pad[i] = k0[i] ^ 0x36;
+	if (halg == 1) {
+		oracle_sha256_init(&c);
+		oracle_sha256_update(&c, pad, bsz);
+		oracle_sha256_update(&c, msg, len);
+		oracle_sha256_final(inner, &c);
+	} else {
+		sha512_init_from(&c, halg == 2 ? iv384 : iv512);
+		oracle_sha512_update(&c, pad, bsz);
+		oracle_sha512_update(&c, msg, len);
+		if (halg == 2)
+			oracle_sha384_final(inner, &c);
+		else
+			oracle_sha512_final(inner, &c);
+	}
+	for (size_t i = 0; i < bsz; i++)
+		pad[i] = k0[i] ^ 0x5c;
+	if (halg == 1) {
+		oracle_sha256_init(&c);
+		oracle_sha256_update(&c, pad, bsz);
+		oracle_sha256_update(&c, inner, dlen);
+		oracle_sha256_final(out, &c);
+	} else {
+		sha512_init_from(&c, halg == 2 ? iv384 : iv512);
+		oracle_sha512_update(&c, pad, bsz);
+		oracle_sha512_update(&c, inner, dlen);
+		if (halg == 2)
+			oracle_sha384_final(out, &c);
+		else
+			oracle_sha512_final(out, &c);
+	}
+	return (int)dlen;
+}

@@ -1,0 +1,134 @@
+"""CPU: the C-ABI library loads, exports every declared entry point, and the
+host-only parts (registry, argument checks) behave like the reference's
+call sites expect.  No kernel is launched here."""
+import ctypes
+import errno
+import os
+import re
+
+import pytest
+
+from ilias_net2_amd import _lib
+from ilias_net2_amd import hash as h
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    names = set()
+    for hdr in ("sha2_batch.h", "hash.h"):
+        src = open(os.path.join(ROOT, "include", "net2", hdr)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names.update(re.findall(r"\b(net2_\w+)\s*\(", src))
+        names.update(re.findall(r"extern\s+const\s+int\s+(net2_\w+)\s*;", src))
+    return names
+
+
+def test_library_builds_and_loads():
+    assert os.path.exists(_lib.LIB_PATH), "run __graft_entry__.build() first"
+    L = _lib.lib()
+    assert L.net2_sha2_abi_version() == 1
+
+
+def test_every_declared_symbol_exported():
+    L = _lib.lib()
+    decl = declared_symbols()
+    assert {"net2_sha2_dev_fixed", "net2_sha2_dev_var", "net2_sha2_batch",
+            "net2_hashctx_hashiov", "net2_hashmax"} <= decl
+    for name in decl:
+        assert hasattr(L, name), name
+    # and the binding declares them all
+    assert decl == set(_lib.SIGNATURES) | set(_lib.DATA_SYMBOLS)
+
+
+def test_registry_rows():
+    # row 0 is nil (connection.c:336, packet.n2t:217 test alg != 0)
+    assert h.hashmax() == 7
+    assert [h.getname(i) for i in range(7)] == [
+        "nil", "SHA256", "SHA384", "SHA512",
+        "HMAC-SHA256", "HMAC-SHA384", "HMAC-SHA512"]
+    assert h.getname(7) is None and h.getname(-1) is None
+    for i in range(7):
+        assert h.findname(h.getname(i)) == i
+    assert h.findname("MD5") == -1
+    assert [h.gethashlen(i) for i in range(7)] == [0, 32, 48, 64, 32, 48, 64]
+    assert [h.getkeylen(i) for i in range(7)] == [0, 0, 0, 0, 32, 48, 64]
+    assert h.gethashlen(99) == -1 and h.getkeylen(99) == -1
+
+
+def _select_sighash(algs):
+    """conn_negotiator.c:189-206 restated: longest unkeyed digest >= 4 B."""
+    sel, best = -1, -1
+    for a in algs:
+        if h.getkeylen(a) != 0:
+            continue
+        hl = h.gethashlen(a)
+        if hl >= 4 and hl > best:
+            sel, best = a, hl
+    return sel
+
+
+def _select_hash(algs):
+    """conn_negotiator.c:110-131 restated: keyed, key >= 16, hash >= 4."""
+    sel, key, hsh = -1, -1, -1
+    for a in algs:
+        k, hl = h.getkeylen(a), h.gethashlen(a)
+        if k >= 16 and hl >= 4 and (k > key or (k == key and hl > hsh)):
+            sel, key, hsh = a, k, hl
+    return sel
+
+
+def test_negotiation_picks():
+    assert _select_sighash(range(h.hashmax())) == 3      # SHA512
+    assert _select_sighash([0, 1]) == 1                  # SHA256
+    assert _select_sighash([0, 4, 5]) == -1              # keyed only
+    assert _select_hash(range(h.hashmax())) == 6         # HMAC-SHA512
+    assert _select_hash([1, 2, 3]) == -1
+
+
+def test_argument_errors_without_launch():
+    L = _lib.lib()
+    buf = ctypes.create_string_buffer(64)
+    # bad alg rows
+    for alg in (-1, 0, 4, 7):
+        assert L.net2_sha2_dev_fixed(alg, buf, 16, 16, 1, buf, None) == errno.EINVAL
+        assert L.net2_sha2_batch(alg, buf, None, None, 16, 16, 1, buf, 0) == errno.EINVAL
+    # n == 0 is a no-op even without a device
+    assert L.net2_sha2_dev_fixed(1, None, 0, 0, 0, None, None) == 0
+    # len > stride with several packets
+    assert L.net2_sha2_dev_fixed(1, buf, 8, 16, 2, buf, None) == errno.EINVAL
+    # var: workspace too small
+    assert L.net2_sha2_dev_var(1, buf, buf, buf, 10, buf, buf, 4, None) == errno.EINVAL
+    # hashiov: unkeyed row given a key (hash-openssl.cc:199-200), keyed row
+    # with a wrong key size (hash-openssl.cc:101), short output
+    iov = (_lib.IOVec * 1)(_lib.IOVec(ctypes.cast(buf, ctypes.c_void_p), 3))
+    assert L.net2_hashctx_hashiov(1, buf, 4, iov, 1, buf, 64) == errno.EINVAL
+    assert L.net2_hashctx_hashiov(4, buf, 16, iov, 1, buf, 64) == errno.EINVAL
+    assert L.net2_hashctx_hashiov(3, None, 0, iov, 1, buf, 32) == errno.EINVAL
+    assert L.net2_hashctx_hashiov(99, None, 0, iov, 1, buf, 64) == errno.EINVAL
+    # nil hashes to nothing
+    assert L.net2_hashctx_hashiov(0, None, 0, iov, 1, None, 0) == 0
+
+
+def test_factory_key_rules():
+    with pytest.raises(ValueError):
+        h.sha256().instantiate(b"k")
+    with pytest.raises(ValueError):
+        h.hmac_sha256().instantiate(b"short")
+    f = h.sha512()
+    assert (f.name, f.hashlen, f.keylen) == ("SHA512", 64, 0)
+
+
+@pytest.mark.skipif(_lib.device_count() > 0, reason="a GPU is present")
+def test_no_device_fails_loudly():
+    """No CPU fallback: compute entry points report ENODEV."""
+    L = _lib.lib()
+    buf = ctypes.create_string_buffer(64)
+    n = ctypes.c_int(-1)
+    assert L.net2_sha2_device_count(ctypes.byref(n)) == errno.ENODEV
+    assert n.value == 0
+    assert L.net2_sha2_dev_fixed(1, buf, 16, 16, 1, buf, None) == errno.ENODEV
+    assert L.net2_sha2_batch(1, buf, None, None, 16, 16, 1, buf, 0) == errno.ENODEV
+    with pytest.raises(_lib.Net2Error) as ei:
+        h.sha256().run(b"", b"abc")
+    assert ei.value.errno == errno.ENODEV

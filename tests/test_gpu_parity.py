@@ -1,0 +1,265 @@
+"""GPU parity: every digest from the HIP path, through the C ABI, equals the
+oracle's (bit-exact) on the same seeded inputs.
+
+Covers the reference's own KATs (test/hash.cc), the boundary lengths where
+SHA256Pad / SHA512Pad change shape (src/sha2.c:495-543, 784-832), empty and
+ragged packets, unaligned packet starts, the length-binned variable path, the
+host-memory end-to-end path, and BASELINE.json's configs at full size
+(1 M x 1 KiB SHA-256 / SHA-512, 1 M x {64, 512, 1500} B) checked
+digest-for-digest against the oracle run on the host cores.
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+import synth
+from golden.make_golden import FIPS_MESSAGES, pattern
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+NAMES = {1: "SHA256", 2: "SHA384", 3: "SHA512"}
+CPU_THREADS = min(16, len(os.sched_getaffinity(0)))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a GPU (HIP device not visible)")
+    from ilias_net2_amd import _lib
+    assert _lib.device_count() >= 1, "no gfx950 device found by the C ABI"
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def batch():
+    from ilias_net2_amd import batch as b
+    return b
+
+
+@pytest.fixture(scope="module")
+def H():
+    from ilias_net2_amd import hash as h
+    return h
+
+
+def to_dev(a: np.ndarray, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def dd(d: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(d).tobytes()).hexdigest()
+
+
+# ---- the reference's C++ hash API (test/hash.cc:50-80), on the GPU ------
+
+def test_reference_hash_cc(dev, H, golden):
+    ref = golden["kat"]["reference"]
+    msg = ref["message"].encode()
+    for fac, name in ((H.sha256(), "SHA256"), (H.sha384(), "SHA384"),
+                      (H.sha512(), "SHA512")):
+        assert fac.run(b"", msg).hex() == ref[name]          # factory.run()
+        ctx = fac.instantiate(b"")                             # instantiate
+        ctx.update(msg)                                        # update
+        assert ctx.final().hex() == ref[name]                  # final
+
+
+def test_fips_and_boundaries_single(dev, H, golden):
+    for key, m in FIPS_MESSAGES.items():
+        for alg, name in NAMES.items():
+            assert H.hashbuf(alg, b"", m).hex() == golden["kat"]["fips"][key][name]
+    for n, row in golden["kat"]["boundary"].items():
+        m = pattern(int(n))
+        for alg, name in NAMES.items():
+            assert H.hashbuf(alg, b"", m).hex() == row[name], (n, name)
+
+
+def test_sha2c_recorded_outputs(dev, H, golden):
+    for n, v in golden["sha2c"]["vectors"].items():
+        m = pattern(int(n))
+        assert H.hashbuf(1, b"", m).hex() == v["SHA256"]
+        assert H.hashbuf(3, b"", m).hex().startswith(v["SHA512_prefix"])
+
+
+def test_iovec_segments(dev, H):
+    """hashbuf over several iovecs == over their concatenation (the
+    SHA256Update-per-iovec loop of src/sign.c:298-304)."""
+    rng = np.random.default_rng(3)
+    m = rng.integers(0, 256, 777, dtype=np.uint8).tobytes()
+    segs = [m[:1], m[1:64], b"", m[64:500], m[500:]]
+    for alg in NAMES:
+        assert H.hashbuf(alg, b"", segs) == H.hashbuf(alg, b"", m)
+
+
+# ---- device-resident fixed layout -----------------------------------------
+
+def test_golden_batches(dev, batch, golden, oracle_mod):
+    for b in golden["batches"]:
+        if b["kind"] == "fixed":
+            data = synth.fixed_batch(b["seed"], b["n"], b["len"], b["stride"])
+            out = batch.digest_fixed(b["alg"], to_dev(data, dev), b["stride"],
+                                     b["len"], b["n"]).cpu().numpy()
+        else:
+            lens = synth.mixed_lengths(b["len_seed"], b["n"])
+            data, offs = synth.packed(b["seed"], lens, align=b["align"])
+            out = batch.digest_var(b["alg"], to_dev(data, dev),
+                                   to_dev(offs.astype(np.int64), dev),
+                                   to_dev(lens.astype(np.int32), dev)).cpu().numpy()
+        assert dd(out) == b["digest_of_digests"], b
+        assert out[0].tobytes().hex() == b["first"]
+
+
+LENGTHS = [0, 1, 3, 55, 56, 57, 63, 64, 65, 111, 112, 113, 119, 120, 127,
+           128, 129, 255, 256, 1000, 1023, 1024, 1500]
+
+
+@pytest.mark.parametrize("alg", [1, 2, 3])
+@pytest.mark.parametrize("stride_kind", ["aligned16", "tight", "odd"])
+def test_fixed_lengths(dev, batch, oracle_mod, alg, stride_kind):
+    for i, length in enumerate(LENGTHS):
+        n = 300 + i  # not a multiple of the 256-lane block
+        stride = {"aligned16": (length + 15) // 16 * 16 or 16,
+                  "tight": max(length, 1),
+                  "odd": length + 3}[stride_kind]
+        data = synth.fixed_batch(100 + i, n, length, stride)
+        got = batch.digest_fixed(alg, to_dev(data, dev), stride, length,
+                                 n).cpu().numpy()
+        want = oracle_mod.batch(alg, data, stride=stride, length=length, n=n,
+                                nthreads=CPU_THREADS)
+        bad = np.nonzero((got != want).any(axis=1))[0]
+        assert bad.size == 0, (alg, stride_kind, length, bad[:8])
+
+
+def test_fixed_unaligned_base(dev, batch, oracle_mod):
+    """A packet batch starting at every byte offset of a dword."""
+    for shift in (1, 2, 3, 5, 8):
+        length, n = 200, 513
+        raw = synth.random_bytes(77 + shift, shift + n * length)
+        t = to_dev(raw, dev)[shift:]
+        for alg in (1, 3):
+            got = batch.digest_fixed(alg, t, length, length, n).cpu().numpy()
+            want = oracle_mod.batch(alg, raw[shift:], stride=length,
+                                    length=length, n=n)
+            assert np.array_equal(got, want), (shift, alg)
+
+
+def test_single_and_empty(dev, batch, oracle_mod):
+    for alg in NAMES:
+        t = torch.zeros(16, dtype=torch.uint8, device=dev)
+        got = batch.digest_fixed(alg, t, 16, 0, 1).cpu().numpy()
+        assert got[0].tobytes() == oracle_mod.digest(alg, b"")
+        t = to_dev(np.frombuffer(b"abc", dtype=np.uint8), dev)
+        got = batch.digest_fixed(alg, t, 3, 3, 1).cpu().numpy()
+        assert got[0].tobytes() == oracle_mod.digest(alg, b"abc")
+
+
+def test_max_payload(dev, batch, oracle_mod):
+    """65,536-byte payloads, the 16-bit carver limit (src/carver.c:150,161)."""
+    n, length = 130, 65536
+    data = synth.fixed_batch(5, n, length)
+    for alg in NAMES:
+        got = batch.digest_fixed(alg, to_dev(data, dev), length, length,
+                                 n).cpu().numpy()
+        want = oracle_mod.batch(alg, data, stride=length, length=length, n=n,
+                                nthreads=CPU_THREADS)
+        assert np.array_equal(got, want), alg
+
+
+# ---- device-resident variable layout (length-binned) ---------------------
+
+@pytest.mark.parametrize("alg", [1, 2, 3])
+@pytest.mark.parametrize("align", [1, 4, 16])
+def test_var_ragged(dev, batch, oracle_mod, alg, align):
+    rng = np.random.default_rng(alg * 31 + align)
+    n = 5000
+    lens = rng.integers(0, 3000, n).astype(np.uint32)
+    lens[:40] = np.array(LENGTHS + LENGTHS[:17], dtype=np.uint32)
+    data, offs = synth.packed(1000 + alg, lens, align=align, gap=1)
+    want = oracle_mod.batch(alg, data, offsets=offs, lens=lens,
+                            nthreads=CPU_THREADS)
+    dt = to_dev(data, dev)
+    do = to_dev(offs.astype(np.int64), dev)
+    dl = to_dev(lens.astype(np.int32), dev)
+    for binned in (True, False):
+        got = batch.digest_var(alg, dt, do, dl, binned=binned).cpu().numpy()
+        bad = np.nonzero((got != want).any(axis=1))[0]
+        assert bad.size == 0, (binned, bad[:8])
+
+
+def test_var_permuted_offsets(dev, batch, oracle_mod):
+    """Offsets need not be sorted or disjoint: shuffled and repeated packets."""
+    rng = np.random.default_rng(9)
+    lens0 = synth.mixed_lengths(9, 3000)
+    data, offs0 = synth.packed(10, lens0)
+    idx = rng.integers(0, 3000, 7000)
+    offs, lens = offs0[idx], lens0[idx]
+    want = oracle_mod.batch(1, data, offsets=offs, lens=lens)
+    got = batch.digest_var(1, to_dev(data, dev), to_dev(offs.astype(np.int64), dev),
+                           to_dev(lens.astype(np.int32), dev)).cpu().numpy()
+    assert np.array_equal(got, want)
+
+
+# ---- host-memory end-to-end path (net2_sha2_batch) ------------------------
+
+def test_host_batch(dev, batch, oracle_mod):
+    data = synth.fixed_batch(21, 20000, 1024)
+    got = batch.digest_host(1, data, stride=1024, length=1024, n=20000)
+    want = oracle_mod.batch(1, data, stride=1024, length=1024, n=20000,
+                            nthreads=CPU_THREADS)
+    assert np.array_equal(got, want)
+    # padded stride, last packet ends exactly at the buffer end
+    n, length, stride = 999, 100, 128
+    data = synth.random_bytes(22, (n - 1) * stride + length)
+    got = batch.digest_host(3, data, stride=stride, length=length, n=n)
+    want = oracle_mod.batch(3, data, stride=stride, length=length, n=n)
+    assert np.array_equal(got, want)
+    # variable layout, unaligned
+    lens = synth.mixed_lengths(23, 30000)
+    data, offs = synth.packed(24, lens)
+    got = batch.digest_host(2, data, offsets=offs, lens=lens)
+    want = oracle_mod.batch(2, data, offsets=offs, lens=lens,
+                            nthreads=CPU_THREADS)
+    assert np.array_equal(got, want)
+
+
+# ---- BASELINE.json configs at full size ------------------------------------
+
+def _full_fixed(dev, batch, oracle_mod, alg, seed):
+    n, length = 1 << 20, 1024
+    data = synth.fixed_batch(seed, n, length)
+    got = batch.digest_fixed(alg, to_dev(data, dev), length, length,
+                             n).cpu().numpy()
+    want = oracle_mod.batch(alg, data, stride=length, length=length, n=n,
+                            nthreads=CPU_THREADS)
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert bad.size == 0, bad[:8]
+
+
+def test_config2_full_sha256(dev, batch, oracle_mod):
+    _full_fixed(dev, batch, oracle_mod, 1, 2)
+
+
+def test_config4_full_sha512(dev, batch, oracle_mod):
+    _full_fixed(dev, batch, oracle_mod, 3, 5)
+
+
+def test_config3_full_mixed(dev, batch, oracle_mod):
+    n = 1 << 20
+    lens = synth.mixed_lengths(3, n)
+    data, offs = synth.packed(4, lens)
+    got = batch.digest_var(1, to_dev(data, dev), to_dev(offs.astype(np.int64), dev),
+                           to_dev(lens.astype(np.int32), dev)).cpu().numpy()
+    want = oracle_mod.batch(1, data, offsets=offs, lens=lens,
+                            nthreads=CPU_THREADS)
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert bad.size == 0, bad[:8]
+
+
+def test_repeat_is_deterministic(dev, batch):
+    data = to_dev(synth.fixed_batch(1, 4096, 1024), dev)
+    a = batch.digest_fixed(1, data, 1024, 1024, 4096)
+    b = batch.digest_fixed(1, data, 1024, 1024, 4096)
+    assert torch.equal(a, b)
