@@ -68,6 +68,21 @@ DATA_SYMBOLS = ("net2_hashmax",)
 _lib = None
 
 
+def _share_torch_hip_runtime() -> None:
+    """One HIP runtime per process.
+
+    PyTorch wheels bundle their own libamdhip64.so (SONAME libamdhip64.so.7,
+    the same SONAME as /opt/rocm's).  If torch is loaded first, the dynamic
+    linker satisfies this library's DT_NEEDED with torch's copy and the
+    process has one runtime; if this library came first, torch would load a
+    second runtime and lose the device.  So when torch is importable, import
+    it before dlopen-ing libnet2_sha2.so.  Pure C callers are unaffected."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def lib() -> ctypes.CDLL:
     """The loaded C ABI; raises if the HIP library was not built."""
     global _lib
@@ -77,6 +92,7 @@ def lib() -> ctypes.CDLL:
                 f"{LIB_PATH} is missing: build it with "
                 "`python -c 'import __graft_entry__ as g; g.build()'` "
                 "(there is no CPU fallback for the SHA-2 path)")
+        _share_torch_hip_runtime()
         handle = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(handle, name)

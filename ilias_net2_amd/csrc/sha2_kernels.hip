@@ -269,6 +269,23 @@ struct PadKW {
 	W kw[sizeof(W) == 4 ? 64 : 80];
 };
 
+/* One lane of the fixed-stride layout: packet i. */
+template <class H, int AMODE, bool PADCONST>
+__device__ __forceinline__ void fixed_lane(uint64_t i,
+    const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
+    uint8_t *__restrict__ out, uint32_t dlen, int is384,
+    const typename H::word *kw)
+{
+	typename H::State st;
+	digest_one<H, AMODE, PADCONST>(base + i * stride, len, is384, kw, st);
+	uint32_t o[16];
+	H::out_words(st, o, is384);
+	if (dlen == 48)
+		store_digest<48>(out + i * 48, o);
+	else
+		store_digest<H::DLEN>(out + i * H::DLEN, o);
+}
+
 template <class H, int AMODE, bool PADCONST>
 __global__ __launch_bounds__(256) void fixed_kernel(const uint8_t *__restrict__ base,
     uint64_t stride, uint32_t len, uint64_t n, uint8_t *__restrict__ out,
@@ -277,15 +294,8 @@ __global__ __launch_bounds__(256) void fixed_kernel(const uint8_t *__restrict__ 
 	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n)
 		return;
-	typename H::State st;
-	digest_one<H, AMODE, PADCONST>(base + i * stride, len, is384, pad.kw,
-	    st);
-	uint32_t o[16];
-	H::out_words(st, o, is384);
-	if (dlen == 48)
-		store_digest<48>(out + i * 48, o);
-	else
-		store_digest<H::DLEN>(out + i * H::DLEN, o);
+	fixed_lane<H, AMODE, PADCONST>(i, base, stride, len, out, dlen, is384,
+	    pad.kw);
 }
 
 /*
@@ -462,6 +472,7 @@ static void pad_kw512(uint64_t bits, PadKW<uint64_t> &p)
 } /* namespace dev */
 } /* namespace net2 */
 
+#ifndef NET2_SHA2_NO_LAUNCHERS
 /* ---- launch wrappers (C++ linkage, used by the C-ABI shim) ------------ */
 
 using namespace net2::dev;
@@ -550,3 +561,4 @@ hipError_t net2_launch_var(int alg, const uint8_t *base,
 		    lens, perm, n, out, dlen, is384);
 	return hipGetLastError();
 }
+#endif /* NET2_SHA2_NO_LAUNCHERS */

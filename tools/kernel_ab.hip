@@ -1,0 +1,113 @@
+// kernel_ab.hip -- launch-shape A/B of the shipped SHA-256 fixed kernel body
+// on the config-2 workload (1M x 1 KiB, device-resident).  All variants run
+// the same lane code (fixed_lane from sha2_kernels.hip); only block size,
+// register attributes and grid shape differ.  Outputs are compared.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I ilias_net2_amd/csrc tools/kernel_ab.hip -o tools/kernel_ab
+#define NET2_SHA2_NO_LAUNCHERS
+#include "../ilias_net2_amd/csrc/sha2_kernels.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+#include <functional>
+
+using namespace net2::dev;
+typedef PadKW<uint32_t> KW;
+
+template <int BS>
+__global__ __launch_bounds__(BS) void k_plain(const uint8_t *base, uint32_t len,
+    uint64_t n, uint8_t *out, KW pad)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+	if (i < n)
+		fixed_lane<Sha256, AMODE_A16, true>(i, base, len, len, out, 32, 0, pad.kw);
+}
+
+template <int BS>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_num_sgpr(80)))
+void k_sgpr80(const uint8_t *base, uint32_t len, uint64_t n, uint8_t *out, KW pad)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
+	if (i < n)
+		fixed_lane<Sha256, AMODE_A16, true>(i, base, len, len, out, 32, 0, pad.kw);
+}
+
+/* grid-stride: gridDim.x blocks loop over the packets */
+template <int BS>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_num_sgpr(80)))
+void k_stride(const uint8_t *base, uint32_t len, uint64_t n, uint8_t *out, KW pad)
+{
+	for (uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x; i < n;
+	    i += (uint64_t)gridDim.x * BS)
+		fixed_lane<Sha256, AMODE_A16, true>(i, base, len, len, out, 32, 0, pad.kw);
+}
+
+template <class F>
+static float best_of(F launch, int reps)
+{
+	hipEvent_t a, b;
+	(void)hipEventCreate(&a);
+	(void)hipEventCreate(&b);
+	float best = 1e9;
+	for (int r = 0; r < reps; r++) {
+		(void)hipEventRecord(a);
+		launch();
+		(void)hipEventRecord(b);
+		(void)hipEventSynchronize(b);
+		float ms;
+		(void)hipEventElapsedTime(&ms, a, b);
+		best = std::min(best, ms);
+	}
+	return best;
+}
+
+int main()
+{
+	const uint64_t n = 1 << 20;
+	const uint32_t len = 1024;
+	uint8_t *d_in, *d_out;
+	(void)hipMalloc(&d_in, n * len);
+	(void)hipMalloc(&d_out, n * 32 * 8);
+	std::vector<uint8_t> h(n * len);
+	uint64_t x = 88172645463325252ull;
+	for (size_t i = 0; i < h.size(); i += 8) {
+		x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+		memcpy(&h[i], &x, 8);
+	}
+	(void)hipMemcpy(d_in, h.data(), h.size(), hipMemcpyHostToDevice);
+	KW pad;
+	pad_kw256((uint64_t)len << 3, pad);
+
+	hipDeviceProp_t p;
+	(void)hipGetDeviceProperties(&p, 0);
+	const int cus = p.multiProcessorCount;
+	struct V { const char *name; std::function<void(uint8_t *)> f; };
+	std::vector<V> vs = {
+		{"A block256 (shipped)", [&](uint8_t *o) { k_plain<256><<<n / 256, 256>>>(d_in, len, n, o, pad); }},
+		{"B block64", [&](uint8_t *o) { k_plain<64><<<n / 64, 64>>>(d_in, len, n, o, pad); }},
+		{"C block128", [&](uint8_t *o) { k_plain<128><<<n / 128, 128>>>(d_in, len, n, o, pad); }},
+		{"D block256 sgpr80", [&](uint8_t *o) { k_sgpr80<256><<<n / 256, 256>>>(d_in, len, n, o, pad); }},
+		{"E block64 sgpr80", [&](uint8_t *o) { k_sgpr80<64><<<n / 64, 64>>>(d_in, len, n, o, pad); }},
+		{"F stride 256x(8/CU) sgpr80", [&](uint8_t *o) { k_stride<256><<<cus * 8, 256>>>(d_in, len, n, o, pad); }},
+		{"G stride 64x(32/CU) sgpr80", [&](uint8_t *o) { k_stride<64><<<cus * 32, 64>>>(d_in, len, n, o, pad); }},
+	};
+	std::vector<float> best(vs.size(), 1e9);
+	for (size_t v = 0; v < vs.size(); v++)
+		vs[v].f(d_out + v * n * 32);  // warm-up
+	(void)hipDeviceSynchronize();
+	for (int round = 0; round < 4; round++)
+		for (size_t v = 0; v < vs.size(); v++)
+			best[v] = std::min(best[v], best_of([&] { vs[v].f(d_out + v * n * 32); }, 3));
+	std::vector<uint8_t> ref(n * 32), got(n * 32);
+	(void)hipMemcpy(ref.data(), d_out, n * 32, hipMemcpyDeviceToHost);
+	printf("{\"n\": %llu, \"len\": %u, \"variants\": [\n", (unsigned long long)n, len);
+	for (size_t v = 0; v < vs.size(); v++) {
+		(void)hipMemcpy(got.data(), d_out + v * n * 32, n * 32, hipMemcpyDeviceToHost);
+		printf("  {\"variant\": \"%s\", \"ms\": %.4f, \"Gdigests_per_s\": %.4f, \"same\": %s}%s\n",
+		    vs[v].name, best[v], n / (best[v] * 1e-3) / 1e9,
+		    got == ref ? "true" : "false", v + 1 == vs.size() ? "" : ",");
+	}
+	printf("]}\n");
+	return 0;
+}
