@@ -92,7 +92,7 @@ def cpu_baseline(cfg):
         best = min(best, time.perf_counter() - t0)
     return {"value": n / best, "unit": "digests/s", "cores": threads,
             "kind": "port",
-            "sample": (f"the full {cfg['workload'].split(',')[0]} batch from host memory, "
+            "sample": (f"the full {cfg['workload'].split(' packets')[0]} packet batch from host memory, "
                        f"oracle/sha2_oracle.c (-O3, rolled transform like src/sha2.c:374-445) "
                        f"on {threads} pthreads, best of 3 after a warm-up")}
 

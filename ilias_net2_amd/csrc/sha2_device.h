@@ -234,14 +234,26 @@ __device__ __forceinline__ void compress256_kw(uint32_t (&st)[8],
 
 /* ---- 64-bit primitives on 32-bit lanes ----------------------------------- */
 
-__device__ __forceinline__ uint32_t lo32(uint64_t x) { return (uint32_t)x; }
+/*
+ * 64-bit words are register pairs.  Halves are moved in and out with
+ * bit casts of a two-lane vector, never with (hi << 32) | lo: written as
+ * shift/or, LLVM re-splits sums of such values into extra v_mov and 64-bit
+ * adds (measured: +10% VALU per SHA-512 block).
+ */
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t lo32(uint64_t x)
+{
+	return __builtin_bit_cast(u32x2, x).x;
+}
 __device__ __forceinline__ uint32_t hi32(uint64_t x)
 {
-	return (uint32_t)(x >> 32);
+	return __builtin_bit_cast(u32x2, x).y;
 }
 __device__ __forceinline__ uint64_t mk64(uint32_t lo, uint32_t hi)
 {
-	return ((uint64_t)hi << 32) | lo;
+	u32x2 v = { lo, hi };
+	return __builtin_bit_cast(uint64_t, v);
 }
 
 /* 64-bit rotate right = two v_alignbit_b32 (halves swap when N >= 32). */
@@ -316,13 +328,79 @@ __device__ __forceinline__ uint64_t expand512(uint64_t (&w)[16])
 	return w[T & 15];
 }
 
+/*
+ * W[t] + K[t] for SHA-512.  NET2_KM512 selects how the 64-bit constant
+ * enters the sum:
+ *   0: plain C -- hipcc parks all 80 constants in SGPR pairs and spills ~100
+ *      SGPRs into VGPR lanes (v_writelane/v_readlane on every block);
+ *   2: a per-workgroup LDS copy of K (k512_lds, filled by
+ *      k512_lds_fill() at kernel entry), read with one broadcast
+ *      ds_read_b64 per round: the constant costs an LDS issue slot instead of
+ *      VALU time or SGPRs.  The read is volatile so it is not hoisted out of
+ *      the block loop (which would pin 160 VGPRs).
+ */
+#ifndef NET2_KM512
+#define NET2_KM512 2
+#endif
+__shared__ uint64_t k512_lds[160];	/* [0,80) K512, [80,160) pad K+W */
+
+/*
+ * Every thread of the workgroup must call one of these before any SHA-512
+ * round.  The padded variant also copies the host-precomputed K[t] + W[t]
+ * of the constant padding block (a kernel argument, 80 64-bit words) to
+ * k512_lds[80 + t]: left in the kernel argument it would be hoisted into 160
+ * SGPRs and spilled.  The argument is read with constant indices only (an
+ * address-taken by-value argument is copied to scratch by hipcc).
+ */
+__device__ __forceinline__ void k512_lds_fill()
+{
+#if NET2_KM512 == 2
+	for (unsigned i = threadIdx.x; i < 80; i += blockDim.x)
+		k512_lds[i] = K512[i];
+	__syncthreads();
+#endif
+}
+
+template <class PAD>
+__device__ __forceinline__ void k512_lds_fill_pad(const PAD &pad)
+{
+#if NET2_KM512 == 2
+	for (unsigned i = threadIdx.x; i < 80; i += blockDim.x)
+		k512_lds[i] = K512[i];
+	if (threadIdx.x < 64) {
+		/* lane l stores pad words l and l + 64 (constant-index reads,
+		 * selected per lane) */
+#pragma unroll
+		for (int t = 0; t < 64; t++)
+			if (threadIdx.x == (unsigned)t)
+				k512_lds[80 + t] = pad.kw[t];
+#pragma unroll
+		for (int t = 64; t < 80; t++)
+			if (threadIdx.x == (unsigned)(t - 64))
+				k512_lds[80 + t] = pad.kw[t];
+	}
+	__syncthreads();
+#endif
+}
+
+template <int T>
+__device__ __forceinline__ uint64_t addk512(uint64_t w)
+{
+#if NET2_KM512 == 2
+	typedef __attribute__((address_space(3))) volatile uint64_t lds_u64;
+	return w + ((lds_u64 *)(k512_lds))[T];
+#else
+	return w + K512[T];
+#endif
+}
+
 template <int T>
 struct Rounds512 {
 	__device__ __forceinline__ static void run(uint64_t (&s)[8],
 	    uint64_t (&w)[16])
 	{
 		uint64_t wt = T < 16 ? w[T & 15] : expand512<T>(w);
-		round512<T>(s, K512[T] + wt);
+		round512<T>(s, addk512<T>(wt));
 		Rounds512<T + 1>::run(s, w);
 	}
 };
@@ -351,7 +429,13 @@ struct RoundsKW512 {
 	__device__ __forceinline__ static void run(uint64_t (&s)[8],
 	    const uint64_t *kw)
 	{
+#if NET2_KM512 == 2
+		typedef __attribute__((address_space(3))) volatile uint64_t lds_u64;
+		round512<T>(s, ((lds_u64 *)(k512_lds))[80 + T]);
+		(void)kw;
+#else
 		round512<T>(s, kw[T]);
+#endif
 		RoundsKW512<T + 1>::run(s, kw);
 	}
 };

@@ -38,6 +38,8 @@ struct Sha256 {
 	static constexpr int NW32 = 16;		/* 32-bit words per block */
 	static constexpr int LENBYTES = 8;	/* trailing length field */
 	static constexpr int DLEN = 32;
+	/* prefetch block k+1 during block k: 16 VGPRs, still 8 waves/SIMD */
+	static constexpr bool PREFETCH = true;
 	typedef uint32_t State[8];
 
 	__device__ __forceinline__ static void init(State &st, int)
@@ -67,6 +69,8 @@ struct Sha512 {
 	static constexpr int NW32 = 32;
 	static constexpr int LENBYTES = 16;
 	static constexpr int DLEN = 64;		/* 48 for SHA-384 */
+	/* a 128-byte prefetch would cost 32 VGPRs and a wave per SIMD */
+	static constexpr bool PREFETCH = false;
 	typedef uint64_t State[8];
 
 	__device__ __forceinline__ static void init(State &st, int is384)
@@ -214,7 +218,7 @@ __device__ __forceinline__ void store_digest(uint8_t *o, const uint32_t (&v)[16]
  * the launch is a multiple of the block size -- the constant padding block
  * whose K[t] + W[t] schedule the host precomputed (kw).
  */
-template <class H, int AMODE, bool PADCONST>
+template <class H, int AMODE, bool PADCONST, bool PREFETCH = H::PREFETCH>
 __device__ __forceinline__ void digest_one(const uint8_t *p, uint32_t len,
     int is384, const typename H::word *kw, typename H::State &st)
 {
@@ -224,18 +228,29 @@ __device__ __forceinline__ void digest_one(const uint8_t *p, uint32_t len,
 
 	H::init(st, is384);
 
-	Raw<NW32> cur;
-	if (nfull > 0)
-		issue_block<NW32, AMODE>(p, cur);
-	for (uint32_t k = 0; k < nfull; k++) {
-		const uint8_t *bp = p + (size_t)k * H::BLOCK;
-		Raw<NW32> nxt;
-		if (k + 1 < nfull)
-			issue_block<NW32, AMODE>(bp + H::BLOCK, nxt);
-		uint32_t w[NW32];
-		finish_block<NW32, AMODE>(bp, cur, w);
-		H::compress(st, w);
-		cur = nxt;
+	if (PREFETCH) {
+		Raw<NW32> cur;
+		if (nfull > 0)
+			issue_block<NW32, AMODE>(p, cur);
+		for (uint32_t k = 0; k < nfull; k++) {
+			const uint8_t *bp = p + (size_t)k * H::BLOCK;
+			Raw<NW32> nxt;
+			if (k + 1 < nfull)
+				issue_block<NW32, AMODE>(bp + H::BLOCK, nxt);
+			uint32_t w[NW32];
+			finish_block<NW32, AMODE>(bp, cur, w);
+			H::compress(st, w);
+			cur = nxt;
+		}
+	} else {
+		for (uint32_t k = 0; k < nfull; k++) {
+			const uint8_t *bp = p + (size_t)k * H::BLOCK;
+			Raw<NW32> cur;
+			issue_block<NW32, AMODE>(bp, cur);
+			uint32_t w[NW32];
+			finish_block<NW32, AMODE>(bp, cur, w);
+			H::compress(st, w);
+		}
 	}
 
 	/* Message length in bits, big-endian, at the end of the last block. */
@@ -270,14 +285,15 @@ struct PadKW {
 };
 
 /* One lane of the fixed-stride layout: packet i. */
-template <class H, int AMODE, bool PADCONST>
+template <class H, int AMODE, bool PADCONST, bool PREFETCH = H::PREFETCH>
 __device__ __forceinline__ void fixed_lane(uint64_t i,
     const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
     uint8_t *__restrict__ out, uint32_t dlen, int is384,
     const typename H::word *kw)
 {
 	typename H::State st;
-	digest_one<H, AMODE, PADCONST>(base + i * stride, len, is384, kw, st);
+	digest_one<H, AMODE, PADCONST, PREFETCH>(base + i * stride, len, is384,
+	    kw, st);
 	uint32_t o[16];
 	H::out_words(st, o, is384);
 	if (dlen == 48)
@@ -292,6 +308,12 @@ __global__ __launch_bounds__(256) void fixed_kernel(const uint8_t *__restrict__ 
     uint32_t dlen, int is384, PadKW<typename H::word> pad)
 {
 	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (sizeof(typename H::word) == 8) {
+		if (PADCONST)
+			k512_lds_fill_pad(pad);
+		else
+			k512_lds_fill();
+	}
 	if (i >= n)
 		return;
 	fixed_lane<H, AMODE, PADCONST>(i, base, stride, len, out, dlen, is384,
@@ -311,6 +333,8 @@ __global__ __launch_bounds__(256) void var_kernel(const uint8_t *__restrict__ ba
     uint32_t dlen, int is384)
 {
 	const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (sizeof(typename H::word) == 8)
+		k512_lds_fill();
 	const bool live = g < n;
 	const uint64_t i = live ? (perm ? (uint64_t)perm[g] : g) : 0;
 	const uint8_t *p = base + (live ? offsets[i] : 0);

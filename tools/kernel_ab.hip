@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <vector>
 #include <functional>
 
@@ -43,6 +44,31 @@ void k_stride(const uint8_t *base, uint32_t len, uint64_t n, uint8_t *out, KW pa
 		fixed_lane<Sha256, AMODE_A16, true>(i, base, len, len, out, 32, 0, pad.kw);
 }
 
+typedef PadKW<uint64_t> KW5;
+
+template <int AM, bool PF>
+__global__ __launch_bounds__(256) void k512(const uint8_t *base, uint32_t len,
+    uint64_t n, uint8_t *out, KW5 pad)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+	k512_lds_fill_pad(pad);
+	if (i < n)
+		fixed_lane<Sha512, AM, true, PF>(i, base, len, len, out, 64, 0, pad.kw);
+}
+
+#define K512V(V)                                                                 \
+	__global__ __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(V)))    \
+	void k512v##V(const uint8_t *base, uint32_t len, uint64_t n, uint8_t *out, KW5 pad) \
+	{                                                                        \
+		const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;     \
+		k512_lds_fill_pad(pad);                                           \
+		if (i < n)                                                       \
+			fixed_lane<Sha512, AMODE_A16, true, false>(i, base, len, len, out, 64, 0, pad.kw); \
+	}
+K512V(96)
+K512V(80)
+K512V(64)
+
 template <class F>
 static float best_of(F launch, int reps)
 {
@@ -68,7 +94,7 @@ int main()
 	const uint32_t len = 1024;
 	uint8_t *d_in, *d_out;
 	(void)hipMalloc(&d_in, n * len);
-	(void)hipMalloc(&d_out, n * 32 * 8);
+	(void)hipMalloc(&d_out, n * 64 * 8);
 	std::vector<uint8_t> h(n * len);
 	uint64_t x = 88172645463325252ull;
 	for (size_t i = 0; i < h.size(); i += 8) {
@@ -78,11 +104,22 @@ int main()
 	(void)hipMemcpy(d_in, h.data(), h.size(), hipMemcpyHostToDevice);
 	KW pad;
 	pad_kw256((uint64_t)len << 3, pad);
+	KW5 pad5;
+	pad_kw512((uint64_t)len << 3, pad5);
+	const bool do512 = getenv("AB512") != nullptr;
 
 	hipDeviceProp_t p;
 	(void)hipGetDeviceProperties(&p, 0);
 	const int cus = p.multiProcessorCount;
 	struct V { const char *name; std::function<void(uint8_t *)> f; };
+	std::vector<V> vs512 = {
+		{"S0 sha512 A16 no-prefetch (shipped)", [&](uint8_t *o) { k512<AMODE_A16, false><<<n / 256, 256>>>(d_in, len, n, o, pad5); }},
+		{"S1 sha512 A16 prefetch", [&](uint8_t *o) { k512<AMODE_A16, true><<<n / 256, 256>>>(d_in, len, n, o, pad5); }},
+		{"S2 sha512 A1 path", [&](uint8_t *o) { k512<AMODE_A1, false><<<n / 256, 256>>>(d_in, len, n, o, pad5); }},
+		{"S3 sha512 A16 vgpr<=96", [&](uint8_t *o) { k512v96<<<n / 256, 256>>>(d_in, len, n, o, pad5); }},
+		{"S4 sha512 A16 vgpr<=80", [&](uint8_t *o) { k512v80<<<n / 256, 256>>>(d_in, len, n, o, pad5); }},
+		{"S5 sha512 A16 vgpr<=64", [&](uint8_t *o) { k512v64<<<n / 256, 256>>>(d_in, len, n, o, pad5); }},
+	};
 	std::vector<V> vs = {
 		{"A block256 (shipped)", [&](uint8_t *o) { k_plain<256><<<n / 256, 256>>>(d_in, len, n, o, pad); }},
 		{"B block64", [&](uint8_t *o) { k_plain<64><<<n / 64, 64>>>(d_in, len, n, o, pad); }},
@@ -92,18 +129,21 @@ int main()
 		{"F stride 256x(8/CU) sgpr80", [&](uint8_t *o) { k_stride<256><<<cus * 8, 256>>>(d_in, len, n, o, pad); }},
 		{"G stride 64x(32/CU) sgpr80", [&](uint8_t *o) { k_stride<64><<<cus * 32, 64>>>(d_in, len, n, o, pad); }},
 	};
+	if (do512)
+		vs = vs512;
+	const int DL = do512 ? 64 : 32;
 	std::vector<float> best(vs.size(), 1e9);
 	for (size_t v = 0; v < vs.size(); v++)
-		vs[v].f(d_out + v * n * 32);  // warm-up
+		vs[v].f(d_out + v * n * DL);  // warm-up
 	(void)hipDeviceSynchronize();
 	for (int round = 0; round < 4; round++)
 		for (size_t v = 0; v < vs.size(); v++)
-			best[v] = std::min(best[v], best_of([&] { vs[v].f(d_out + v * n * 32); }, 3));
-	std::vector<uint8_t> ref(n * 32), got(n * 32);
-	(void)hipMemcpy(ref.data(), d_out, n * 32, hipMemcpyDeviceToHost);
+			best[v] = std::min(best[v], best_of([&] { vs[v].f(d_out + v * n * DL); }, 3));
+	std::vector<uint8_t> ref(n * DL), got(n * DL);
+	(void)hipMemcpy(ref.data(), d_out, n * DL, hipMemcpyDeviceToHost);
 	printf("{\"n\": %llu, \"len\": %u, \"variants\": [\n", (unsigned long long)n, len);
 	for (size_t v = 0; v < vs.size(); v++) {
-		(void)hipMemcpy(got.data(), d_out + v * n * 32, n * 32, hipMemcpyDeviceToHost);
+		(void)hipMemcpy(got.data(), d_out + v * n * DL, n * DL, hipMemcpyDeviceToHost);
 		printf("  {\"variant\": \"%s\", \"ms\": %.4f, \"Gdigests_per_s\": %.4f, \"same\": %s}%s\n",
 		    vs[v].name, best[v], n / (best[v] * 1e-3) / 1e9,
 		    got == ref ? "true" : "false", v + 1 == vs.size() ? "" : ",");
