@@ -202,12 +202,21 @@ def main():
             "algorithmic_bytes_per_launch": per_launch}
     valu = None
     if pmc and pmc.get("valu_wave_instr_per_launch"):
-        rate = pmc["valu_wave_instr_per_launch"] / (launch_ms / 1e3)
+        instr = pmc["valu_wave_instr_per_launch"]
+        rate = instr / (launch_ms / 1e3)
+        clk = pmc.get("clock_ghz_under_pmc") or 2.4
         valu = {"bound": "valu", "achieved": round(rate / 1e12, 4),
                 "peak": round(VALU_PEAK_WAVE_INSTR / 1e12, 4),
                 "unit": "T wave64-VALU-instr/s",
                 "frac": round(rate / VALU_PEAK_WAVE_INSTR, 4),
-                "source": "rocprofv3 SQ_INSTS_VALU, profiles/pmc_%s.json" % args.config}
+                # SIMD cycles between VALU issues, averaged over the launch:
+                # 2.0 = the nominal SIMD-32 rate; tools/valu_probe measured
+                # ~4.1 for v_alignbit/v_add3/v_perm and ~3.5 for v_bitop3,
+                # which make up >90% of the SHA rounds
+                "simd_cycles_per_valu_instr": round(clk * 1e9 * (launch_ms / 1e3) * 1024 / instr, 3),
+                "clock_ghz": round(clk, 3),
+                "instr_per_launch": instr,
+                "source": "rocprofv3 SQ_INSTS_VALU / GRBM_GUI_ACTIVE, profiles/pmc_%s.json" % args.config}
 
     line = {
         "metric": METRIC if args.config == "c2" else

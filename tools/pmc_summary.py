@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""Fold rocprofv3 outputs into the per-launch numbers bench.py reports.
+
+Inputs (produced by tools/gpu_profile.sh on the GPU box, one rocprofv3 call
+per counter group -- PMC passes are never combined with tracing):
+  gpurun_out/prof_<cfg>/run_kernel_stats.csv            --kernel-trace --stats
+  gpurun_out/pmc_<cfg>_<group>/run_counter_collection.csv   --pmc <group>
+
+Output: profiles/pmc_<cfg>.json and a copy of the kernel-stats CSV under
+profiles/<round>/.
+
+Corrections (MI355X_MICROARCH.md, "HBM" and "rocprofv3 PMC slots"):
+  * FETCH_SIZE / WRITE_SIZE are in KiB; x1024 for bytes.
+  * gfx950 FETCH_SIZE counts exactly half the bytes of a 16 B/lane read
+    stream (128-B requests tallied as 64 B): our block loads are
+    global_load_dwordx4 (16 B/lane), so FETCH_SIZE is doubled.
+  * WRITE_SIZE is exact for 16 B/lane stores (digests are dwordx4 stores).
+  * GRBM_GUI_ACTIVE is summed over the 8 XCDs: clock = value / 8 / duration.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import shutil
+import statistics
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = {"c2": "fixed_kernel<net2::dev::Sha256", "c4": "fixed_kernel<net2::dev::Sha512",
+          "c3": "var_kernel<net2::dev::Sha256"}
+
+
+def per_dispatch(path, pattern):
+    """{counter: [per-dispatch totals]} and [durations ns] for one kernel."""
+    vals, durs = {}, {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if pattern not in r["Kernel_Name"]:
+                continue
+            d = r["Dispatch_Id"]
+            key = (d, r["Counter_Name"])
+            vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
+            durs[d] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    out = {}
+    for (d, c), v in vals.items():
+        out.setdefault(c, []).append(v)
+    return out, list(durs.values())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cfg", required=True, choices=sorted(KERNEL))
+    ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
+    ap.add_argument("--round", default="round1")
+    args = ap.parse_args()
+    pat = KERNEL[args.cfg]
+
+    counters, durs_all = {}, []
+    for path in sorted(glob.glob(os.path.join(args.src, f"pmc_{args.cfg}_*", "run_counter_collection.csv"))):
+        c, d = per_dispatch(path, pat)
+        for k, v in c.items():
+            counters[k] = v
+        durs_all += d
+    med = {k: statistics.median(v) for k, v in counters.items()}
+    res = {"config": args.cfg, "kernel": pat, "dispatches_per_pass": len(durs_all) and
+           max(len(v) for v in counters.values()),
+           "counters_median_per_launch": med}
+    stats_csv = os.path.join(args.src, f"prof_{args.cfg}", "run_kernel_stats.csv")
+    if os.path.exists(stats_csv):
+        with open(stats_csv) as f:
+            for r in csv.DictReader(f):
+                if pat in r["Name"]:
+                    res["trace_avg_ns"] = float(r["AverageNs"])
+                    res["trace_calls"] = int(r["Calls"])
+        dst = os.path.join(ROOT, "profiles", args.round)
+        os.makedirs(dst, exist_ok=True)
+        shutil.copy(stats_csv, os.path.join(dst, f"kernel_stats_{args.cfg}.csv"))
+    if "FETCH_SIZE" in med:
+        fetch = med["FETCH_SIZE"] * 1024 * 2          # KiB -> B, gfx950 x2
+        write = med.get("WRITE_SIZE", 0.0) * 1024
+        res["hbm_read_bytes_per_launch"] = fetch
+        res["hbm_write_bytes_per_launch"] = write
+        res["hbm_bytes_per_launch"] = fetch + write
+        res["correction"] = "FETCH_SIZE*1024*2 (gfx950 16B/lane half-count) + WRITE_SIZE*1024"
+    if "SQ_INSTS_VALU" in med:
+        res["valu_wave_instr_per_launch"] = med["SQ_INSTS_VALU"]
+    if "GRBM_GUI_ACTIVE" in med and durs_all:
+        res["clock_ghz_under_pmc"] = med["GRBM_GUI_ACTIVE"] / 8 / statistics.median(durs_all)
+    out = os.path.join(ROOT, "profiles", f"pmc_{args.cfg}.json")
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1, sort_keys=True)
+    print(json.dumps(res, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main()
