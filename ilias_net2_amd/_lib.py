@@ -61,7 +61,8 @@ SIGNATURES = {
     "net2_hmac_dev": (ctypes.c_int, [
         ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
-        ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+        ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+        ctypes.c_void_p]),
 }
 DATA_SYMBOLS = ("net2_hashmax",)
 

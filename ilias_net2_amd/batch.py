@@ -96,3 +96,30 @@ def digest_host(alg: int, data: np.ndarray, offsets: Optional[np.ndarray] = None
                                     _np_ptr(out), max_devices)
     check(rc, "net2_sha2_batch")
     return out
+
+
+def hmac_dev(alg: int, key: bytes, data, stride: int = 0, length: int = 0,
+             n: Optional[int] = None, offsets=None, lens=None, out=None,
+             binned: bool = True, stream=None):
+    """Batched HMAC (registry rows 4..6) of device-resident packets under one
+    key: fixed layout (stride/length/n) or variable layout (offsets/lens)."""
+    import torch
+    dl = DIGEST_LEN[alg]
+    if offsets is not None:
+        n = int(offsets.numel())
+    if out is None:
+        out = torch.empty((n, dl), dtype=torch.uint8, device=data.device)
+    kb = ctypes.create_string_buffer(bytes(key), max(len(key), 1))
+    ws_ptr, ws_bytes = None, 0
+    if offsets is not None and binned and n:
+        ws = var_workspace(n, data.device)
+        ws_ptr, ws_bytes = ws.data_ptr(), ws.numel() * 4
+    rc = _lib.lib().net2_hmac_dev(
+        alg, kb, len(key), data.data_ptr(),
+        None if offsets is None else offsets.data_ptr(),
+        None if lens is None else lens.data_ptr(), stride, length, n,
+        out.data_ptr(), ws_ptr, ws_bytes, _stream_ptr(stream))
+    check(rc, "net2_hmac_dev")
+    if ws_ptr is not None:
+        torch.cuda.current_stream(data.device).synchronize()
+    return out

@@ -218,15 +218,17 @@ __device__ __forceinline__ void store_digest(uint8_t *o, const uint32_t (&v)[16]
  * the launch is a multiple of the block size -- the constant padding block
  * whose K[t] + W[t] schedule the host precomputed (kw).
  */
-template <class H, int AMODE, bool PADCONST, bool PREFETCH = H::PREFETCH>
-__device__ __forceinline__ void digest_one(const uint8_t *p, uint32_t len,
-    int is384, const typename H::word *kw, typename H::State &st)
+/*
+ * SHA*Update over the len / BLOCK full blocks at p (src/sha2.c:477-485:
+ * whole blocks are transformed straight from caller memory).  With
+ * PREFETCH, block k+1 is loaded while block k is compressed.
+ */
+template <class H, int AMODE, bool PREFETCH = H::PREFETCH>
+__device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
+    typename H::State &st)
 {
 	constexpr int NW32 = H::NW32;
 	const uint32_t nfull = len / H::BLOCK;
-	const uint32_t rem = len % H::BLOCK;
-
-	H::init(st, is384);
 
 	if (PREFETCH) {
 		Raw<NW32> cur;
@@ -252,9 +254,20 @@ __device__ __forceinline__ void digest_one(const uint8_t *p, uint32_t len,
 			H::compress(st, w);
 		}
 	}
+}
 
-	/* Message length in bits, big-endian, at the end of the last block. */
-	const uint64_t bits = (uint64_t)len << 3;
+/*
+ * SHA*Pad (src/sha2.c:495-543 / :784-832): the len % BLOCK tail bytes, the
+ * 0x80 terminator, zero fill and the big-endian bit count `bits` (the whole
+ * message, including any prefix hashed before p), in one or two blocks.
+ * PADCONST: the caller knows len % BLOCK == 0 for every lane, so the pad
+ * block is constant and its K[t] + W[t] schedule comes precomputed in kw.
+ */
+template <class H, bool PADCONST>
+__device__ __forceinline__ void finish(const uint8_t *p, uint32_t len,
+    uint64_t bits, const typename H::word *kw, typename H::State &st)
+{
+	constexpr int NW32 = H::NW32;
 	if (PADCONST) {
 		if (sizeof(typename H::word) == 4)
 			compress256_kw(*reinterpret_cast<uint32_t(*)[8]>(&st),
@@ -264,6 +277,8 @@ __device__ __forceinline__ void digest_one(const uint8_t *p, uint32_t len,
 			    reinterpret_cast<const uint64_t *>(kw));
 		return;
 	}
+	const uint32_t nfull = len / H::BLOCK;
+	const uint32_t rem = len % H::BLOCK;
 	uint32_t w[NW32];
 	tail_block<NW32>(p + (size_t)nfull * H::BLOCK, rem, w);
 	if (rem >= (uint32_t)(H::BLOCK - H::LENBYTES)) {
@@ -278,7 +293,17 @@ __device__ __forceinline__ void digest_one(const uint8_t *p, uint32_t len,
 	H::compress(st, w);
 }
 
-/* Constant-pad schedule passed by value (kernarg -> SGPRs). */
+/* Init + Update + Pad of one whole message (Final's store is the caller's). */
+template <class H, int AMODE, bool PADCONST, bool PREFETCH = H::PREFETCH>
+__device__ __forceinline__ void digest_one(const uint8_t *p, uint32_t len,
+    int is384, const typename H::word *kw, typename H::State &st)
+{
+	H::init(st, is384);
+	absorb<H, AMODE, PREFETCH>(p, len, st);
+	finish<H, PADCONST>(p, len, (uint64_t)len << 3, kw, st);
+}
+
+/* Constant-pad schedule passed by value (kernarg -> SGPRs / LDS). */
 template <class W>
 struct PadKW {
 	W kw[sizeof(W) == 4 ? 64 : 80];
@@ -353,6 +378,145 @@ __global__ __launch_bounds__(256) void var_kernel(const uint8_t *__restrict__ ba
 		store_digest<48>(out + i * 48, o);
 	else
 		store_digest<H::DLEN>(out + i * H::DLEN, o);
+}
+
+/* ---- HMAC (RFC 2104) ------------------------------------------------------ */
+
+/*
+ * The keyed rows of the registry (HMAC-SHA256/384/512, key length = digest
+ * length, cxx_src/hash-openssl.cc:417-429), i.e. the per-datagram
+ * authenticator of net2_packet_encode/decode (types/packet.n2t:246,417),
+ * over a whole batch under one connection key:
+ *   HMAC(K, m) = H((K' ^ opad) || H((K' ^ ipad) || m)),  K' = K zero-padded.
+ * The two key blocks are compressed once per workgroup (wave 0, wave-
+ * uniform) into LDS midstates; every lane then hashes its packet from the
+ * inner midstate (bit count includes the key block) and finishes with one
+ * outer compression over the inner digest.
+ */
+template <int NW32>
+struct HKey {
+	uint32_t w[NW32];	/* K' as big-endian words */
+};
+
+/* The state as big-endian digest words (SHA*Final's byte order). */
+template <class H>
+__device__ __forceinline__ int digest_words(const typename H::State &st,
+    int is384, uint32_t (&w)[H::NW32])
+{
+	if (sizeof(typename H::word) == 4) {
+#pragma unroll
+		for (int i = 0; i < 8; i++)
+			w[i] = (uint32_t)st[i];
+		return 8;
+	}
+#pragma unroll
+	for (int i = 0; i < 8; i++) {
+		w[2 * i] = hi32((uint64_t)st[i]);
+		w[2 * i + 1] = lo32((uint64_t)st[i]);
+	}
+	return is384 ? 12 : 16;
+}
+
+template <class H>
+__device__ __forceinline__ void hmac_lane(const uint8_t *p, uint32_t len,
+    int is384, bool a16, const uint32_t (*mid)[16], typename H::State &st)
+{
+	constexpr int NW32 = H::NW32;
+	typename H::State outer;
+#pragma unroll
+	for (int i = 0; i < 8; i++) {
+		if (sizeof(typename H::word) == 4) {
+			st[i] = mid[0][i];
+			outer[i] = mid[1][i];
+		} else {
+			st[i] = mk64(mid[0][2 * i + 1], mid[0][2 * i]);
+			outer[i] = mk64(mid[1][2 * i + 1], mid[1][2 * i]);
+		}
+	}
+	if (a16)
+		absorb<H, AMODE_A16>(p, len, st);
+	else
+		absorb<H, AMODE_A1>(p, len, st);
+	finish<H, false>(p, len, ((uint64_t)len + H::BLOCK) << 3, nullptr, st);
+
+	/* outer: one block = inner digest || 0x80 || 0... || bit count */
+	uint32_t w[NW32];
+#pragma unroll
+	for (int i = 0; i < NW32; i++)
+		w[i] = 0;
+	const int dw = digest_words<H>(st, is384, w);
+#pragma unroll
+	for (int i = 12; i < 16; i++)		/* SHA-384 keeps 12 words */
+		if (i >= dw)
+			w[i] = 0;
+	w[dw] = 0x80000000u;
+	const uint64_t obits = (uint64_t)(H::BLOCK + 4 * dw) << 3;
+	w[NW32 - 2] = (uint32_t)(obits >> 32);
+	w[NW32 - 1] = (uint32_t)obits;
+#pragma unroll
+	for (int i = 0; i < 8; i++)
+		st[i] = outer[i];
+	H::compress(st, w);
+}
+
+template <class H>
+__global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ base,
+    const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
+    const uint32_t *__restrict__ perm, uint64_t stride, uint32_t fixed_len,
+    uint64_t n, uint8_t *__restrict__ out, uint32_t dlen, int is384,
+    HKey<H::NW32> key)
+{
+	constexpr int NW32 = H::NW32;
+	__shared__ uint32_t mid[2][16];
+	if (sizeof(typename H::word) == 8)
+		k512_lds_fill();
+	if (threadIdx.x < 64) {
+#pragma unroll
+		for (int pass = 0; pass < 2; pass++) {
+			const uint32_t pad = pass ? 0x5c5c5c5cu : 0x36363636u;
+			typename H::State ks;
+			H::init(ks, is384);
+			uint32_t w[NW32];
+#pragma unroll
+			for (int i = 0; i < NW32; i++)
+				w[i] = key.w[i] ^ pad;
+			H::compress(ks, w);
+			uint32_t kw[NW32];
+			digest_words<H>(ks, 0, kw);
+			if (threadIdx.x == 0)
+#pragma unroll
+				for (int i = 0; i < 16; i++)
+					mid[pass][i] = i < (sizeof(typename H::word) == 4 ? 8 : 16) ? kw[i] : 0u;
+		}
+	}
+	__syncthreads();
+
+	const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	const bool live = g < n;
+	uint64_t i = g;
+	const uint8_t *p;
+	uint32_t len;
+	if (offsets != nullptr) {
+		i = live ? (perm ? (uint64_t)perm[g] : g) : 0;
+		p = base + (live ? offsets[i] : 0);
+		len = live ? lens[i] : 0;
+	} else {
+		p = base + (live ? i * stride : 0);
+		len = live ? fixed_len : 0;
+	}
+	typename H::State st;
+	hmac_lane<H>(p, len, is384,
+	    __all((reinterpret_cast<uintptr_t>(p) & 15) == 0), mid, st);
+	if (!live)
+		return;
+	uint32_t o[16];
+	H::out_words(st, o, is384);
+	if (dlen == 48)
+		store_digest<48>(out + i * 48, o);
+	else if (dlen == 32)
+		store_digest<32>(out + i * 32, o);
+	else
+		store_digest<64>(out + i * 64, o);
 }
 
 /* ---- length binning (counting sort by block count, longest first) ---- */
@@ -547,6 +711,30 @@ hipError_t net2_launch_fixed(int alg, const uint8_t *base, uint64_t stride,
 	return hipGetLastError();
 }
 
+/* Length-binned visiting order of a variable-length batch into ws. */
+hipError_t net2_bin_order(int alg, const uint32_t *lens, uint64_t n,
+    uint32_t *ws, hipStream_t s)
+{
+	const bool s256 = alg == NET2_ALG_SHA256;
+	const int blk_shift = s256 ? 6 : 7;
+	const int lenbytes = s256 ? 8 : 16;
+	uint32_t *hist = ws;
+	uint32_t *cursor = ws + NET2_SHA2_NBINS;
+	uint32_t *perm = ws + 2 * NET2_SHA2_NBINS;
+	hipError_t e = hipMemsetAsync(hist, 0, NET2_SHA2_NBINS * sizeof(uint32_t),
+	    s);
+	if (e != hipSuccess)
+		return e;
+	unsigned g = grid_for(n);
+	if (g > 2048)
+		g = 2048;
+	bin_count_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift, lenbytes, hist);
+	bin_scan_kernel<<<1, 1024, 0, s>>>(hist, cursor);
+	bin_scatter_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift, lenbytes, cursor,
+	    perm);
+	return hipGetLastError();
+}
+
 hipError_t net2_launch_var(int alg, const uint8_t *base,
     const uint64_t *offsets, const uint32_t *lens, uint64_t n, uint8_t *out,
     uint32_t *ws, hipStream_t s)
@@ -561,21 +749,10 @@ hipError_t net2_launch_var(int alg, const uint8_t *base,
 	uint32_t *perm = nullptr;
 
 	if (ws != nullptr) {
-		uint32_t *hist = ws;
-		uint32_t *cursor = ws + NET2_SHA2_NBINS;
-		perm = ws + 2 * NET2_SHA2_NBINS;
-		hipError_t e = hipMemsetAsync(hist, 0,
-		    NET2_SHA2_NBINS * sizeof(uint32_t), s);
+		hipError_t e = net2_bin_order(alg, lens, n, ws, s);
 		if (e != hipSuccess)
 			return e;
-		unsigned g = grid_for(n);
-		if (g > 2048)
-			g = 2048;
-		bin_count_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift, lenbytes,
-		    hist);
-		bin_scan_kernel<<<1, 1024, 0, s>>>(hist, cursor);
-		bin_scatter_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift,
-		    lenbytes, cursor, perm);
+		perm = ws + 2 * NET2_SHA2_NBINS;
 	}
 	if (s256)
 		var_kernel<Sha256><<<grid_for(n), 256, 0, s>>>(base, offsets,
@@ -583,6 +760,48 @@ hipError_t net2_launch_var(int alg, const uint8_t *base,
 	else
 		var_kernel<Sha512><<<grid_for(n), 256, 0, s>>>(base, offsets,
 		    lens, perm, n, out, dlen, is384);
+	return hipGetLastError();
+}
+hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
+    const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
+    uint64_t stride, uint32_t fixed_len, uint64_t n, uint8_t *out,
+    uint32_t *ws, hipStream_t s)
+{
+	if (n == 0)
+		return hipSuccess;
+	const int halg = alg - 3;	/* HMAC row -> SHA row */
+	const bool s256 = halg == NET2_ALG_SHA256;
+	const int blk = s256 ? 64 : 128;
+	const int is384 = halg == NET2_ALG_SHA384;
+	const uint32_t dlen = s256 ? 32 : is384 ? 48 : 64;
+	uint8_t kb[128] = { 0 };
+	if (keylen > (size_t)blk)
+		return hipErrorInvalidValue;	/* registry keys are <= a block */
+	for (size_t i = 0; i < keylen; i++)
+		kb[i] = key[i];
+	uint32_t *perm = nullptr;
+	if (offsets != nullptr && ws != nullptr) {
+		hipError_t e = net2_bin_order(halg, lens, n, ws, s);
+		if (e != hipSuccess)
+			return e;
+		perm = ws + 2 * NET2_SHA2_NBINS;
+	}
+	const unsigned grid = grid_for(n);
+	if (s256) {
+		HKey<16> k;
+		for (int i = 0; i < 16; i++)
+			k.w[i] = ((uint32_t)kb[4 * i] << 24) | ((uint32_t)kb[4 * i + 1] << 16) |
+			    ((uint32_t)kb[4 * i + 2] << 8) | kb[4 * i + 3];
+		hmac_kernel<Sha256><<<grid, 256, 0, s>>>(base, offsets, lens, perm,
+		    stride, fixed_len, n, out, dlen, 0, k);
+	} else {
+		HKey<32> k;
+		for (int i = 0; i < 32; i++)
+			k.w[i] = ((uint32_t)kb[4 * i] << 24) | ((uint32_t)kb[4 * i + 1] << 16) |
+			    ((uint32_t)kb[4 * i + 2] << 8) | kb[4 * i + 3];
+		hmac_kernel<Sha512><<<grid, 256, 0, s>>>(base, offsets, lens, perm,
+		    stride, fixed_len, n, out, dlen, is384, k);
+	}
 	return hipGetLastError();
 }
 #endif /* NET2_SHA2_NO_LAUNCHERS */

@@ -32,4 +32,18 @@ hipError_t net2_launch_var(int alg, const uint8_t *base,
     const uint64_t *offsets, const uint32_t *lens, uint64_t n, uint8_t *out,
     uint32_t *ws, hipStream_t s);
 
+/* Length-binned order (ws as above; perm = ws + 2 * NBINS). */
+hipError_t net2_bin_order(int alg, const uint32_t *lens, uint64_t n,
+    uint32_t *ws, hipStream_t s);
+
+/*
+ * HMAC batch (alg = 4..6).  key/keylen in host memory (keylen <= block);
+ * offsets == NULL selects the fixed layout (stride, fixed_len); ws as for
+ * net2_launch_var (may be NULL).
+ */
+hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
+    const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
+    uint64_t stride, uint32_t fixed_len, uint64_t n, uint8_t *out,
+    uint32_t *ws, hipStream_t s);
+
 #endif /* NET2_SHA2_LAUNCH_H */

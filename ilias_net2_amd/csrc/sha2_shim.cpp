@@ -329,7 +329,8 @@ int run_device_slice(size_t didx, int alg, const uint8_t *base,
 }
 
 /* Single message, gathered from iovecs, on the first device. */
-int hash_small(int alg, const struct iovec *iov, size_t iovcnt, uint8_t *out)
+int hash_small(int alg, const uint8_t *key, size_t keylen,
+    const struct iovec *iov, size_t iovcnt, uint8_t *out)
 {
 	size_t total = 0;
 	for (size_t i = 0; i < iovcnt; i++)
@@ -354,8 +355,13 @@ int hash_small(int alg, const struct iovec *iov, size_t iovcnt, uint8_t *out)
 	const int dl = digest_len(alg);
 	HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, std::max<size_t>(total, 1),
 	    hipMemcpyHostToDevice, s.stream));
-	HIP_TRY(net2_launch_fixed(alg, s.d_in, std::max<size_t>(total, 16),
-	    (uint32_t)total, 1, s.d_dig, s.stream));
+	if (unkeyed_sha2(alg))
+		HIP_TRY(net2_launch_fixed(alg, s.d_in, std::max<size_t>(total, 16),
+		    (uint32_t)total, 1, s.d_dig, s.stream));
+	else
+		HIP_TRY(net2_launch_hmac(alg, key, keylen, s.d_in, nullptr,
+		    nullptr, std::max<size_t>(total, 16), (uint32_t)total, 1,
+		    s.d_dig, nullptr, s.stream));
 	HIP_TRY(hipMemcpyAsync(s.h_dig, s.d_dig, dl, hipMemcpyDeviceToHost,
 	    s.stream));
 	HIP_TRY(hipStreamSynchronize(s.stream));
@@ -559,19 +565,41 @@ NET2_EXPORT int net2_hashctx_hashiov(int alg, const void *key, size_t keylen,
 		return EINVAL;
 	if (devices().empty())
 		return ENODEV;
-	if (!unkeyed_sha2(alg))
-		return ENOSYS;	/* keyed rows: see net2_hmac_dev */
-	return hash_small(alg, iov, iovcnt, (uint8_t *)out);
+	return hash_small(alg, (const uint8_t *)key, keylen, iov, iovcnt,
+	    (uint8_t *)out);
 }
 
 NET2_EXPORT int net2_hmac_dev(int alg, const void *key, size_t keylen,
     const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
     uint64_t stride, uint32_t fixed_len, uint64_t n, void *d_digests,
-    void *stream)
+    void *d_ws, size_t ws_bytes, void *stream)
 {
-	(void)key; (void)keylen; (void)d_base; (void)d_offsets; (void)d_lens;
-	(void)stride; (void)fixed_len; (void)n; (void)d_digests; (void)stream;
 	if (alg < NET2_HASH_HMAC_SHA256 || alg > NET2_HASH_HMAC_SHA512)
 		return EINVAL;
-	return ENOSYS;
+	if ((size_t)kRows[alg].keylen != keylen || key == nullptr)
+		return EINVAL;
+	if (n == 0)
+		return 0;
+	if (d_digests == nullptr)
+		return EINVAL;
+	if (d_offsets != nullptr) {
+		if (d_lens == nullptr)
+			return EINVAL;
+		if (d_ws != nullptr && (ws_bytes < net2_sha2_dev_var_workspace(n) ||
+		    ((uintptr_t)d_ws & 3) != 0 || n > UINT32_MAX))
+			return EINVAL;
+	} else {
+		if (d_base == nullptr && fixed_len > 0)
+			return EINVAL;
+		if (n > 1 && stride < fixed_len)
+			return EINVAL;
+	}
+	int rc = check_current_device();
+	if (rc != 0)
+		return rc;
+	HIP_TRY(net2_launch_hmac(alg, (const uint8_t *)key, keylen,
+	    (const uint8_t *)d_base, d_offsets, d_lens, stride, fixed_len, n,
+	    (uint8_t *)d_digests, d_offsets ? (uint32_t *)d_ws : nullptr,
+	    (hipStream_t)stream));
+	return 0;
 }

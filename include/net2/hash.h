@@ -66,15 +66,18 @@ int net2_hashctx_hashiov(int alg, const void *key, size_t keylen,
 /*
  * Batched keyed hash (HMAC, RFC 2104) of many packets under one key -- the
  * per-datagram authenticator of net2_packet_encode/decode
- * (types/packet.n2t:246,417) for a whole receive batch.  Layouts as
- * net2_sha2_dev_fixed / net2_sha2_dev_var (d_offsets == NULL: fixed).
- * alg is an HMAC row; keylen must equal its key length.  Asynchronous on
+ * (types/packet.n2t:246,417) for a whole receive or transmit batch.
+ * alg is an HMAC row (4..6); keylen must equal its key length; key is host
+ * memory.  Layouts as net2_sha2_dev_fixed (d_offsets == NULL: packet i at
+ * d_base + i * stride, fixed_len bytes) or net2_sha2_dev_var (d_offsets /
+ * d_lens, optional binning workspace d_ws of net2_sha2_dev_var_workspace(n)
+ * bytes).  Digests (hashlen bytes each) to d_digests.  Asynchronous on
  * stream.
  */
 int net2_hmac_dev(int alg, const void *key, size_t keylen,
     const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
     uint64_t stride, uint32_t fixed_len, uint64_t n, void *d_digests,
-    void *stream);
+    void *d_ws, size_t ws_bytes, void *stream);
 
 #ifdef __cplusplus
 }

@@ -263,3 +263,49 @@ def test_repeat_is_deterministic(dev, batch):
     a = batch.digest_fixed(1, data, 1024, 1024, 4096)
     b = batch.digest_fixed(1, data, 1024, 1024, 4096)
     assert torch.equal(a, b)
+
+
+# ---- HMAC rows ------------------------------------------
+
+def test_hmac_single(dev, H, golden):
+    """net2_hashctx_hashiov on keyed rows == the golden HMAC vectors
+    (oracle + Python hmac agree on them)."""
+    facs = {4: H.hmac_sha256(), 5: H.hmac_sha384(), 6: H.hmac_sha512()}
+    for v in golden["kat"]["hmac"]:
+        key = bytes.fromhex(v["key"])
+        assert facs[v["alg"]].run(key, pattern(v["len"])).hex() == v["digest"]
+        ctx = facs[v["alg"]].instantiate(key)
+        ctx.update(pattern(v["len"]))
+        assert ctx.final().hex() == v["digest"]
+
+
+@pytest.mark.parametrize("alg", [4, 5, 6])
+def test_hmac_batches(dev, batch, oracle_mod, alg):
+    import hmac as pyhmac
+    hl = {4: 32, 5: 48, 6: 64}[alg]
+    key = bytes(synth.random_bytes(40 + alg, hl))
+    # fixed layout across the padding boundaries
+    for length in (0, 1, 55, 56, 64, 111, 112, 128, 1000, 1024):
+        n = 257
+        stride = length + 5
+        data = synth.fixed_batch(50 + length, n, length, stride)
+        got = batch.hmac_dev(alg, key, to_dev(data, dev), stride=stride,
+                             length=length, n=n).cpu().numpy()
+        for i in (0, 1, n // 2, n - 1):
+            msg = data[i * stride:i * stride + length].tobytes()
+            assert got[i].tobytes() == oracle_mod.hmac(alg, key, msg), (length, i)
+        h = {4: "sha256", 5: "sha384", 6: "sha512"}[alg]
+        msg = data[:length].tobytes()
+        assert got[0].tobytes() == pyhmac.new(key, msg, h).digest()
+    # variable layout (MTU-sized datagrams), binned and not
+    lens = synth.mixed_lengths(60 + alg, 3000, choices=(64, 512, 1500, 1472, 20))
+    data, offs = synth.packed(61 + alg, lens)
+    want = np.stack([np.frombuffer(oracle_mod.hmac(
+        alg, key, data[int(o):int(o) + int(l)].tobytes()), dtype=np.uint8)
+        for o, l in zip(offs, lens)])
+    for binned in (True, False):
+        got = batch.hmac_dev(alg, key, to_dev(data, dev),
+                             offsets=to_dev(offs.astype(np.int64), dev),
+                             lens=to_dev(lens.astype(np.int32), dev),
+                             binned=binned).cpu().numpy()
+        assert np.array_equal(got, want), binned
