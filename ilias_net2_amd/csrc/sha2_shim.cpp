@@ -213,13 +213,47 @@ DeviceCtx *ctx_for(size_t idx)
 /* Chunk payload target for the host pipeline. */
 constexpr size_t kChunkBytes = 64u << 20;
 
+/* Page-locked (pinned or registered) host memory can be DMA'd directly. */
+bool is_pinned(const void *p)
+{
+	hipPointerAttribute_t a;
+	if (p == nullptr || hipPointerGetAttributes(&a, p) != hipSuccess) {
+		(void)hipGetLastError();	/* clear the sticky lookup error */
+		return false;
+	}
+	return a.type == hipMemoryTypeHost;
+}
+
+/* memcpy of a large range split over a few threads (staging copies). */
+void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes)
+{
+	const size_t piece = 8u << 20;
+	const size_t nt = std::min<size_t>(8, (bytes + piece - 1) / piece);
+	if (nt <= 1) {
+		memcpy(dst, src, bytes);
+		return;
+	}
+	std::vector<std::thread> th;
+	for (size_t t = 1; t < nt; t++) {
+		size_t a = bytes * t / nt, b = bytes * (t + 1) / nt;
+		th.emplace_back([=]() { memcpy(dst + a, src + a, b - a); });
+	}
+	memcpy(dst, src, bytes / nt);
+	for (std::thread &x : th)
+		x.join();
+}
+
 /*
- * Gather one chunk [lo, hi) of the caller's packets into slot s (packed,
- * 16-byte aligned packet starts), enqueue H2D + kernel + D2H.
+ * One chunk [lo, hi) of the caller's packets into slot s: H2D (straight from
+ * the caller's buffer when it is pinned and the layout is fixed, else
+ * through the slot's pinned staging, packed with 16-byte aligned packet
+ * starts), kernel, D2H of the digests (straight into the caller's buffer
+ * when that is pinned).
  */
 int enqueue_chunk(Slot &s, int alg, const uint8_t *base,
     const uint64_t *offsets, const uint32_t *lens, uint64_t stride,
-    uint32_t fixed_len, uint64_t lo, uint64_t hi, uint8_t *user_dig)
+    uint32_t fixed_len, uint64_t lo, uint64_t hi, uint8_t *user_dig,
+    bool src_pinned, bool dst_pinned)
 {
 	const uint64_t n = hi - lo;
 	const int dl = digest_len(alg);
@@ -227,7 +261,8 @@ int enqueue_chunk(Slot &s, int alg, const uint8_t *base,
 	int rc;
 
 	if (offsets == nullptr) {
-		bytes = (size_t)n * ((fixed_len + 15) & ~15u);
+		bytes = src_pinned ? (size_t)(n - 1) * stride + fixed_len
+		    : (size_t)n * ((fixed_len + 15) & ~15u);
 	} else {
 		for (uint64_t i = lo; i < hi; i++)
 			bytes += ((size_t)lens[i] + 15) & ~(size_t)15;
@@ -235,12 +270,17 @@ int enqueue_chunk(Slot &s, int alg, const uint8_t *base,
 	if ((rc = s.reserve(bytes, n)) != 0)
 		return rc;
 
-	if (offsets == nullptr) {
+	if (offsets == nullptr && src_pinned) {
+		HIP_TRY(hipMemcpyAsync(s.d_in, base + lo * stride, bytes,
+		    hipMemcpyHostToDevice, s.stream));
+		HIP_TRY(net2_launch_fixed(alg, s.d_in, stride, fixed_len, n,
+		    s.d_dig, s.stream));
+	} else if (offsets == nullptr) {
 		const size_t st = (fixed_len + 15) & ~15u;
 		if (st == stride) {
 			/* contiguous; the caller's buffer ends at the last
 			 * packet's last byte, not at a stride boundary */
-			memcpy(s.h_in, base + lo * stride,
+			par_memcpy(s.h_in, base + lo * stride,
 			    (size_t)(n - 1) * stride + fixed_len);
 		} else {
 			for (uint64_t i = 0; i < n; i++)
@@ -269,11 +309,11 @@ int enqueue_chunk(Slot &s, int alg, const uint8_t *base,
 		HIP_TRY(net2_launch_var(alg, s.d_in, s.d_off, s.d_len, n,
 		    s.d_dig, n >= 4096 ? s.d_ws : nullptr, s.stream));
 	}
-	HIP_TRY(hipMemcpyAsync(s.h_dig, s.d_dig, (size_t)n * dl,
-	    hipMemcpyDeviceToHost, s.stream));
+	HIP_TRY(hipMemcpyAsync(dst_pinned ? user_dig : s.h_dig, s.d_dig,
+	    (size_t)n * dl, hipMemcpyDeviceToHost, s.stream));
 	HIP_TRY(hipEventRecord(s.done, s.stream));
 	s.busy = true;
-	s.user_dig = user_dig;
+	s.user_dig = dst_pinned ? nullptr : user_dig;
 	s.user_bytes = (size_t)n * dl;
 	return 0;
 }
@@ -284,7 +324,8 @@ int drain(Slot &s)
 		return 0;
 	s.busy = false;
 	HIP_TRY(hipEventSynchronize(s.done));
-	memcpy(s.user_dig, s.h_dig, s.user_bytes);
+	if (s.user_dig != nullptr)
+		memcpy(s.user_dig, s.h_dig, s.user_bytes);
 	return 0;
 }
 
@@ -299,6 +340,8 @@ int run_device_slice(size_t didx, int alg, const uint8_t *base,
 	int rc = 0, cur = 0;
 
 	HIP_TRY(hipSetDevice(devices()[didx]));
+	const bool src_pinned = offsets == nullptr && is_pinned(base);
+	const bool dst_pinned = is_pinned(digests);
 	for (uint64_t at = lo; at < hi && rc == 0;) {
 		/* chunk end: at most kChunkBytes of (padded) payload */
 		uint64_t end = at;
@@ -319,7 +362,8 @@ int run_device_slice(size_t didx, int alg, const uint8_t *base,
 		if ((rc = drain(s)) != 0)
 			break;
 		rc = enqueue_chunk(s, alg, base, offsets, lens, stride,
-		    fixed_len, at, end, digests + at * dl);
+		    fixed_len, at, end, digests + at * dl, src_pinned,
+		    dst_pinned);
 		at = end;
 		cur ^= 1;
 	}

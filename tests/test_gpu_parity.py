@@ -216,6 +216,17 @@ def test_host_batch(dev, batch, oracle_mod):
     got = batch.digest_host(3, data, stride=stride, length=length, n=n)
     want = oracle_mod.batch(3, data, stride=stride, length=length, n=n)
     assert np.array_equal(got, want)
+    # pinned (page-locked) source and destination: direct DMA path
+    n, length, stride = 70001, 1000, 1008
+    src = torch.from_numpy(synth.random_bytes(25, (n - 1) * stride + length)).pin_memory()
+    out = torch.empty((n, 32), dtype=torch.uint8).pin_memory()
+    from ilias_net2_amd import _lib
+    rc = _lib.lib().net2_sha2_batch(1, src.data_ptr(), None, None, stride,
+                                    length, n, out.data_ptr(), 0)
+    assert rc == 0
+    want = oracle_mod.batch(1, src.numpy(), stride=stride, length=length, n=n,
+                            nthreads=CPU_THREADS)
+    assert np.array_equal(out.numpy(), want)
     # variable layout, unaligned
     lens = synth.mixed_lengths(23, 30000)
     data, offs = synth.packed(24, lens)
