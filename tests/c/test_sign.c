@@ -1,0 +1,297 @@
+/*
+ * test_sign.c -- C-level test of the signed-payload path over the MI355X
+ * hash ABI.  Part 1 restates the reference's test/sign.c:57-185 (P-521 key
+ * pair from test/sign.c:27-45): sign a maxmsglen message, validate it, a
+ * second signature differs, a tampered message is invalid, pubkey(priv) ==
+ * pubkey(pub).  Part 2 checks the hash-then-sign objects of
+ * types/signature.n2t and their batched forms: every digest the GPU feeds to
+ * ECDSA is checked independently by verifying the signature against an
+ * OpenSSL-computed digest of the same payload (OpenSSL here is the test's
+ * independent reference, never the product path).
+ *
+ * Usage: test_sign <priv.pem> <pub.pem> [all|cpu]; exit 0 = pass.  "all"
+ * (default) needs a GPU; "cpu" runs only part 1, which hashes nothing.
+ */
+#include "../../include/net2/hash.h"
+#include "../../include/net2/sign.h"
+#include "../../include/net2/signature.h"
+
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <openssl/evp.h>
+#include <openssl/pem.h>
+
+static int failures;
+
+#define CHECK(cond) do {							\
+	if (!(cond)) {							\
+		fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__,	\
+		    #cond);						\
+		failures++;						\
+	}								\
+} while (0)
+
+static char *
+slurp(const char *path, size_t *len)
+{
+	FILE *f = fopen(path, "rb");
+	char *buf;
+	long n;
+
+	if (f == NULL)
+		return NULL;
+	fseek(f, 0, SEEK_END);
+	n = ftell(f);
+	fseek(f, 0, SEEK_SET);
+	buf = malloc((size_t)n + 1);
+	if (buf == NULL || fread(buf, 1, (size_t)n, f) != (size_t)n) {
+		fclose(f);
+		free(buf);
+		return NULL;
+	}
+	fclose(f);
+	buf[n] = 0;
+	*len = (size_t)n;
+	return buf;
+}
+
+static uint64_t rng_state = 0x9E3779B97F4A7C15ull;
+
+static uint8_t
+rnd8(void)
+{
+	rng_state ^= rng_state << 13;
+	rng_state ^= rng_state >> 7;
+	rng_state ^= rng_state << 17;
+	return (uint8_t)rng_state;
+}
+
+/* Independent reference digest (OpenSSL EVP), test-only. */
+static void
+ref_digest(int alg, const uint8_t *m, size_t len, uint8_t *out)
+{
+	const EVP_MD *md = alg == 1 ? EVP_sha256() : alg == 2 ? EVP_sha384()
+	    : EVP_sha512();
+	unsigned int ol = 0;
+
+	EVP_Digest(m, len, out, &ol, md, NULL);
+}
+
+static int
+ref_verify(EVP_PKEY *pub, const uint8_t *sig, size_t siglen,
+    const uint8_t *dig, size_t dlen)
+{
+	EVP_PKEY_CTX *pc = EVP_PKEY_CTX_new(pub, NULL);
+	int ok = pc && EVP_PKEY_verify_init(pc) == 1 &&
+	    EVP_PKEY_verify(pc, sig, siglen, dig, dlen) == 1;
+
+	EVP_PKEY_CTX_free(pc);
+	return ok;
+}
+
+/* Part 1: test/sign.c restated. */
+static void
+test_reference_flow(struct net2_sign_ctx *priv, struct net2_sign_ctx *pub)
+{
+	size_t maxlen = net2_signctx_maxmsglen(priv);
+	uint8_t *msg = malloc(maxlen), *sig = malloc(maxlen),
+	    *sig2 = malloc(maxlen);
+	size_t siglen = maxlen, sig2len = maxlen;
+	uint8_t pk1[256], pk2[256];
+	size_t pk1len = sizeof(pk1), pk2len = sizeof(pk2);
+
+	CHECK(maxlen > 0);
+	for (size_t i = 0; i < maxlen; i++)
+		msg[i] = rnd8();
+	CHECK(net2_signctx_sign(priv, msg, maxlen, sig, &siglen) == 0);
+	CHECK(net2_signctx_validate(pub, sig, siglen, msg, maxlen) == 1);
+	/* a second signature of the same message differs (random k) */
+	CHECK(net2_signctx_sign(priv, msg, maxlen, sig2, &sig2len) == 0);
+	CHECK(siglen != sig2len || memcmp(sig, sig2, siglen) != 0);
+	CHECK(net2_signctx_validate(pub, sig2, sig2len, msg, maxlen) == 1);
+	/* tampered message is invalid (test/sign.c:129-148) */
+	msg[0] ^= 0xff;
+	msg[1] ^= 0x5a;
+	CHECK(net2_signctx_validate(pub, sig, siglen, msg, maxlen) == 0);
+	/* a public context cannot sign */
+	CHECK(net2_signctx_sign(pub, msg, maxlen, sig2, &sig2len) == EINVAL);
+	/* public keys agree (test/sign.c:151-180) */
+	CHECK(net2_signctx_pubkey(priv, pk1, &pk1len) == 0);
+	CHECK(net2_signctx_pubkey(pub, pk2, &pk2len) == 0);
+	CHECK(pk1len == pk2len && memcmp(pk1, pk2, pk1len) == 0);
+	CHECK(pk1len == 133 && pk1[0] == 0x04);	/* uncompressed P-521 */
+	CHECK(strcmp(net2_signctx_name(priv), "ecdsa") == 0);
+	CHECK(net2_sign_findname("ecdsa") == 0 && net2_sign_getname(1) == NULL);
+	free(msg);
+	free(sig);
+	free(sig2);
+}
+
+/* Fingerprint = SHA-256 of the uncompressed point (src/sign.c:258-320). */
+static void
+test_fingerprint(struct net2_sign_ctx *priv, struct net2_sign_ctx *pub)
+{
+	uint8_t fp1[32], fp2[32], want[32], pk[256];
+	size_t pklen = sizeof(pk);
+	struct net2_sign_ctx *clone;
+
+	CHECK(net2_signctx_fingerprint(priv, fp1) == 0);
+	CHECK(net2_signctx_fingerprint(pub, fp2) == 0);
+	CHECK(memcmp(fp1, fp2, 32) == 0);
+	CHECK(net2_signctx_pubkey(pub, pk, &pklen) == 0);
+	ref_digest(1, pk, pklen, want);
+	CHECK(memcmp(fp1, want, 32) == 0);
+	clone = net2_signctx_clone(pub);
+	CHECK(clone != NULL);
+	CHECK(net2_signctx_fingerprint(clone, fp2) == 0 &&
+	    memcmp(fp2, want, 32) == 0);
+	net2_signctx_free(clone);
+}
+
+/* Part 2: signature objects, single and batched. */
+static void
+test_signatures(struct net2_sign_ctx *priv, struct net2_sign_ctx *pub,
+    EVP_PKEY *refpub)
+{
+	enum { N = 1000 };
+	static const uint32_t shapes[] = { 0, 1, 64, 111, 112, 512, 1024, 1500,
+	    65536 };
+	uint64_t offs[N];
+	uint32_t lens[N];
+	size_t total = 0;
+	uint8_t *buf, dig[64];
+	struct net2_signature one, *many;
+	struct iovec iov[3];
+	int valid, *vv;
+
+	for (int i = 0; i < N; i++) {
+		lens[i] = shapes[i % 9] == 65536 && i > 9 ? 777 : shapes[i % 9];
+		offs[i] = total;
+		total += lens[i] + (i & 3);	/* ragged, unaligned */
+	}
+	buf = malloc(total + 1);
+	for (size_t i = 0; i < total; i++)
+		buf[i] = rnd8();
+
+	/* single, scattered over three iovecs (signature.n2t:60-119) */
+	iov[0].iov_base = buf;
+	iov[0].iov_len = 100;
+	iov[1].iov_base = buf + 100;
+	iov[1].iov_len = 0;
+	iov[2].iov_base = buf + 100;
+	iov[2].iov_len = 1400;
+	for (int alg = 1; alg <= 3; alg++) {
+		CHECK(net2_signature_create(&one, iov, 3, alg, priv) == 0);
+		CHECK(strcmp(one.hash_alg, net2_hash_getname(alg)) == 0);
+		CHECK(strcmp(one.sign_alg, "ecdsa") == 0);
+		CHECK(net2_signature_validate(&one, iov, 3, pub, &valid) == 0 &&
+		    valid == 1);
+		ref_digest(alg, buf, 1500, dig);
+		CHECK(ref_verify(refpub, one.data, one.datalen, dig,
+		    (size_t)net2_hash_gethashlen(alg)));
+		buf[700] ^= 1;				/* tamper */
+		CHECK(net2_signature_validate(&one, iov, 3, pub, &valid) == 0 &&
+		    valid == 0);
+		buf[700] ^= 1;
+		net2_signature_deinit(&one);
+	}
+	/* error behaviour of signature.n2t:69-72, 133-158 */
+	CHECK(net2_signature_create(&one, iov, 3, 0, priv) == EINVAL);
+	CHECK(net2_signature_create(&one, iov, 3, 4, priv) == EINVAL);
+	CHECK(net2_signature_create(&one, iov, 3, 99, priv) == EINVAL);
+	CHECK(net2_signature_create(&one, iov, 3, 3, priv) == 0);
+	free(one.hash_alg);
+	one.hash_alg = strdup("MD5");
+	CHECK(net2_signature_validate(&one, iov, 3, pub, &valid) == EOPNOTSUPP &&
+	    valid == 0);
+	free(one.hash_alg);
+	one.hash_alg = strdup("SHA512");
+	free(one.sign_alg);
+	one.sign_alg = strdup("rsa");
+	CHECK(net2_signature_validate(&one, iov, 3, pub, &valid) == EINVAL);
+	net2_signature_deinit(&one);
+	CHECK(net2_signature_validate(NULL, iov, 3, pub, &valid) == EINVAL);
+
+	/* batched: one GPU hash launch for all N payloads, then ECDSA */
+	many = calloc(N, sizeof(*many));
+	vv = calloc(N, sizeof(*vv));
+	CHECK(net2_signature_create_batch(many, buf, offs, lens, N, 3, priv,
+	    8) == 0);
+	for (int i = 0; i < N; i += 37) {
+		ref_digest(3, buf + offs[i], lens[i], dig);
+		CHECK(ref_verify(refpub, many[i].data, many[i].datalen, dig, 64));
+	}
+	CHECK(net2_signature_validate_batch(many, buf, offs, lens, N, pub, vv,
+	    8) == 0);
+	for (int i = 0; i < N; i++)
+		CHECK(vv[i] == 1);
+	/* mixed hash algorithms and broken entries in one validate batch */
+	net2_signature_deinit(&many[5]);
+	CHECK(net2_signature_create(&many[5], &(struct iovec){ buf + offs[5],
+	    lens[5] }, 1, 1, priv) == 0);		/* SHA256 entry */
+	free(many[6].hash_alg);
+	many[6].hash_alg = strdup("MD5");		/* unknown hash */
+	buf[offs[7]] ^= 0x80;				/* tampered payload */
+	CHECK(lens[7] > 0);
+	CHECK(net2_signature_validate_batch(many, buf, offs, lens, N, pub, vv,
+	    4) == 0);
+	for (int i = 0; i < N; i++)
+		CHECK(vv[i] == (i == 6 || i == 7 ? 0 : 1));
+	for (int i = 0; i < N; i++)
+		net2_signature_deinit(&many[i]);
+	free(many);
+	free(vv);
+	free(buf);
+}
+
+int
+main(int argc, char **argv)
+{
+	char *privpem, *pubpem;
+	size_t privlen, publen;
+	struct net2_sign_ctx *priv, *pub;
+	EVP_PKEY *refpub;
+	BIO *bio;
+	int ndev = 0;
+
+	int cpu_only = argc == 4 && strcmp(argv[3], "cpu") == 0;
+
+	if (argc != 3 && argc != 4) {
+		fprintf(stderr, "usage: %s priv.pem pub.pem [all|cpu]\n", argv[0]);
+		return 2;
+	}
+	if (!cpu_only && (net2_sha2_device_count(&ndev) != 0 || ndev < 1)) {
+		fprintf(stderr, "no gfx950 device\n");
+		return 3;
+	}
+	privpem = slurp(argv[1], &privlen);
+	pubpem = slurp(argv[2], &publen);
+	if (privpem == NULL || pubpem == NULL)
+		return 2;
+	priv = net2_signctx_privnew(0, privpem, privlen);
+	pub = net2_signctx_pubnew(0, pubpem, publen);
+	CHECK(priv != NULL && pub != NULL);
+	CHECK(net2_signctx_pubnew(1, pubpem, publen) == NULL);	/* bad alg */
+	CHECK(net2_signctx_privnew(0, pubpem, publen) == NULL);	/* not priv */
+	bio = BIO_new_mem_buf(pubpem, (int)publen);
+	refpub = PEM_read_bio_PUBKEY(bio, NULL, NULL, NULL);
+	BIO_free(bio);
+	if (priv && pub && refpub) {
+		test_reference_flow(priv, pub);
+		if (!cpu_only) {
+			test_fingerprint(priv, pub);
+			test_signatures(priv, pub, refpub);
+		}
+	}
+	EVP_PKEY_free(refpub);
+	net2_signctx_free(priv);
+	net2_signctx_free(pub);
+	free(privpem);
+	free(pubpem);
+	printf("%s%s (%d failures)\n", failures ? "FAIL" : "PASS",
+	    cpu_only ? " cpu-only" : "", failures);
+	return failures ? 1 : 0;
+}
