@@ -519,6 +519,56 @@ __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ b
 		store_digest<64>(out + i * 64, o);
 }
 
+/* ---- packet-header IV derivation (types/packet.n2t:100-158) ---------------- */
+
+/*
+ * iv = first ivlen bytes of D0 || D1 with D0 = SHA-256(ph), D1 = SHA-256(ph
+ * || D0), ph = be32(seq) || be32(flags) (cp_packet_header,
+ * packet.n2t:89-95).  The reference loops until the IV is long enough;
+ * ivlen <= 64 covers two rounds, each a single block (8 + 32 bytes < 56).
+ */
+__global__ __launch_bounds__(256) void ph_iv_kernel(const uint32_t *__restrict__ seq,
+    const uint32_t *__restrict__ flags, uint64_t n, uint32_t ivlen,
+    uint8_t *__restrict__ out)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n)
+		return;
+	const uint32_t s = seq[i], f = flags[i];
+	uint32_t d[16];
+	uint32_t st[8], w[16];
+#pragma unroll
+	for (int r = 0; r < 2; r++) {
+		if (r == 1 && ivlen <= 32)
+			break;
+#pragma unroll
+		for (int j = 0; j < 16; j++)
+			w[j] = 0;
+		w[0] = s;
+		w[1] = f;
+		if (r == 0) {
+			w[2] = 0x80000000u;
+			w[15] = 8 * 8;
+		} else {
+#pragma unroll
+			for (int j = 0; j < 8; j++)
+				w[2 + j] = d[j];
+			w[10] = 0x80000000u;
+			w[15] = 40 * 8;
+		}
+#pragma unroll
+		for (int j = 0; j < 8; j++)
+			st[j] = IV256[j];
+		compress256(st, w);
+#pragma unroll
+		for (int j = 0; j < 8; j++)
+			d[8 * r + j] = st[j];
+	}
+	uint8_t *o = out + i * ivlen;
+	for (uint32_t b = 0; b < ivlen; b++)
+		o[b] = (uint8_t)(d[b >> 2] >> (24 - 8 * (b & 3)));
+}
+
 /* ---- length binning (counting sort by block count, longest first) ---- */
 
 __device__ __forceinline__ uint32_t bin_of(uint32_t len, int blk_shift,
@@ -802,6 +852,16 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 		hmac_kernel<Sha512><<<grid, 256, 0, s>>>(base, offsets, lens, perm,
 		    stride, fixed_len, n, out, dlen, is384, k);
 	}
+	return hipGetLastError();
+}
+hipError_t net2_launch_ph_iv(const uint32_t *seq, const uint32_t *flags,
+    uint64_t n, uint32_t ivlen, uint8_t *out, hipStream_t s)
+{
+	if (n == 0 || ivlen == 0)
+		return hipSuccess;
+	if (ivlen > 64)
+		return hipErrorInvalidValue;
+	ph_iv_kernel<<<grid_for(n), 256, 0, s>>>(seq, flags, n, ivlen, out);
 	return hipGetLastError();
 }
 #endif /* NET2_SHA2_NO_LAUNCHERS */

@@ -46,4 +46,8 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
     uint64_t stride, uint32_t fixed_len, uint64_t n, uint8_t *out,
     uint32_t *ws, hipStream_t s);
 
+/* Packet-header IVs (ivlen <= 64): out = n x ivlen bytes. */
+hipError_t net2_launch_ph_iv(const uint32_t *seq, const uint32_t *flags,
+    uint64_t n, uint32_t ivlen, uint8_t *out, hipStream_t s);
+
 #endif /* NET2_SHA2_LAUNCH_H */

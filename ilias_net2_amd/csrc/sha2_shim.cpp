@@ -29,6 +29,7 @@
 #define NET2_EXPORT extern "C" __attribute__((visibility("default")))
 
 #include "../../include/net2/hash.h"
+#include "../../include/net2/packet.h"
 
 namespace {
 
@@ -644,6 +645,50 @@ NET2_EXPORT int net2_hmac_dev(int alg, const void *key, size_t keylen,
 	HIP_TRY(net2_launch_hmac(alg, (const uint8_t *)key, keylen,
 	    (const uint8_t *)d_base, d_offsets, d_lens, stride, fixed_len, n,
 	    (uint8_t *)d_digests, d_offsets ? (uint32_t *)d_ws : nullptr,
+	    (hipStream_t)stream));
+	return 0;
+}
+
+NET2_EXPORT int net2_ph_to_iv(const struct net2_packet_header *ph,
+    size_t ivlen, void *iv)
+{
+	uint8_t hdr[8];
+	uint8_t *out = (uint8_t *)iv;
+	uint8_t d[32];
+	size_t have = 0;
+
+	if (ph == nullptr || (iv == nullptr && ivlen > 0))
+		return EINVAL;
+	for (int i = 0; i < 4; i++) {
+		hdr[i] = (uint8_t)(ph->seq >> (24 - 8 * i));
+		hdr[4 + i] = (uint8_t)(ph->flags >> (24 - 8 * i));
+	}
+	while (have < ivlen) {		/* packet.n2t:127-144 */
+		struct iovec v[2] = { { hdr, sizeof(hdr) }, { out, have } };
+		int rc = net2_hashctx_hashiov(NET2_HASH_SHA256, nullptr, 0, v, 2,
+		    d, sizeof(d));
+		if (rc != 0)
+			return rc;
+		size_t take = std::min<size_t>(32, ivlen - have);
+		memcpy(out + have, d, take);
+		have += take;
+	}
+	return 0;
+}
+
+NET2_EXPORT int net2_ph_to_iv_dev(const uint32_t *d_seq,
+    const uint32_t *d_flags, uint64_t n, uint32_t ivlen, void *d_iv,
+    void *stream)
+{
+	if (n == 0 || ivlen == 0)
+		return 0;
+	if (ivlen > 64 || d_seq == nullptr || d_flags == nullptr ||
+	    d_iv == nullptr)
+		return EINVAL;
+	int rc = check_current_device();
+	if (rc != 0)
+		return rc;
+	HIP_TRY(net2_launch_ph_iv(d_seq, d_flags, n, ivlen, (uint8_t *)d_iv,
 	    (hipStream_t)stream));
 	return 0;
 }

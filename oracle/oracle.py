@@ -48,6 +48,8 @@ def lib() -> ctypes.CDLL:
                                         ctypes.c_uint64, ctypes.c_uint32, sz,
                                         vp, ctypes.c_int]
         L.oracle_sha2_batch.restype = ctypes.c_int
+        L.oracle_ph_to_iv.argtypes = [ctypes.c_uint32, ctypes.c_uint32, sz, vp]
+        L.oracle_ph_to_iv.restype = ctypes.c_int
         for pfx in ("sha256", "sha384", "sha512"):
             for fn, args in (("init", [vp]), ("update", [vp, vp, sz]),
                              ("pad", [vp]), ("final", [vp, vp])):
@@ -95,3 +97,9 @@ def batch(alg: int, data: np.ndarray, offsets=None, lens=None, stride=0,
     if rc != 0:
         raise ValueError(f"bad alg {alg}")
     return out
+
+
+def ph_to_iv(seq: int, flags: int, ivlen: int) -> bytes:
+    out = ctypes.create_string_buffer(max(ivlen, 1))
+    lib().oracle_ph_to_iv(seq, flags, ivlen, out)
+    return out.raw[:ivlen]

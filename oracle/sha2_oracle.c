@@ -493,3 +493,28 @@ int oracle_hmac_digest(int alg, const uint8_t *key, size_t keylen,
 	}
 	return (int)dlen;
 }
+
+/* ---- net2_ph_to_iv (types/packet.n2t:100-158) --------------------------- */
+
+int oracle_ph_to_iv(uint32_t seq, uint32_t flags, size_t ivlen, uint8_t *iv)
+{
+	uint8_t ph[8], d[32];
+	size_t have = 0;
+	oracle_sha2_ctx c;
+
+	/* cp_packet_header: uint32 seq, uint32 flags, big-endian
+	 * (packet.n2t:89-95, include/ilias/net2/cp.h:197-205) */
+	store_be32(ph, seq);
+	store_be32(ph + 4, flags);
+	/* iv += SHA256(ph || iv) until long enough (packet.n2t:127-144) */
+	while (have < ivlen) {
+		size_t take = ivlen - have < 32 ? ivlen - have : 32;
+		oracle_sha256_init(&c);
+		oracle_sha256_update(&c, ph, 8);
+		oracle_sha256_update(&c, iv, have);
+		oracle_sha256_final(d, &c);
+		memcpy(iv + have, d, take);
+		have += take;
+	}
+	return 0;
+}

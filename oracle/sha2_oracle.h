@@ -88,6 +88,13 @@ int oracle_sha2_batch(int alg, const uint8_t *base, const uint64_t *offsets,
 int oracle_hmac_digest(int alg, const uint8_t *key, size_t keylen,
     const uint8_t *msg, size_t len, uint8_t *out);
 
+/*
+ * IV derivation from a packet header (types/packet.n2t:100-158): the header
+ * encoded as two big-endian uint32 (seq, flags); iv grows by SHA-256(ph ||
+ * iv) until it holds ivlen bytes.
+ */
+int oracle_ph_to_iv(uint32_t seq, uint32_t flags, size_t ivlen, uint8_t *iv);
+
 #ifdef __cplusplus
 }
 #endif

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_symbols():
     names = set()
-    for hdr in ("sha2_batch.h", "hash.h"):
+    for hdr in ("sha2_batch.h", "hash.h", "packet.h"):
         src = open(os.path.join(ROOT, "include", "net2", hdr)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         names.update(re.findall(r"\b(net2_\w+)\s*\(", src))

@@ -320,3 +320,39 @@ def test_hmac_batches(dev, batch, oracle_mod, alg):
                              lens=to_dev(lens.astype(np.int32), dev),
                              binned=binned).cpu().numpy()
         assert np.array_equal(got, want), binned
+
+
+# ---- net2_ph_to_iv (types/packet.n2t:100-158) -------------
+
+def test_ph_to_iv(dev, oracle_mod):
+    import ctypes
+    from ilias_net2_amd import _lib
+    L = _lib.lib()
+
+    class PH(ctypes.Structure):
+        _fields_ = [("seq", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+    # single-header form, any ivlen (the reference loop)
+    for seq, flags in ((0, 0), (1, 2), (0xFFFFFFFF, 0x80000001)):
+        for ivlen in (0, 1, 16, 31, 32, 33, 64, 65, 100):
+            out = ctypes.create_string_buffer(max(ivlen, 1))
+            assert L.net2_ph_to_iv(ctypes.byref(PH(seq, flags)), ivlen, out) == 0
+            assert out.raw[:ivlen] == oracle_mod.ph_to_iv(seq, flags, ivlen)
+    # batched device form
+    n = 100003
+    rng = np.random.default_rng(17)
+    seq = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    flags = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    ds = to_dev(seq.view(np.int32), dev)
+    df = to_dev(flags.view(np.int32), dev)
+    for ivlen in (16, 32, 48, 64):
+        out = torch.empty(n * ivlen, dtype=torch.uint8, device=dev)
+        rc = L.net2_ph_to_iv_dev(ds.data_ptr(), df.data_ptr(), n, ivlen,
+                                 out.data_ptr(),
+                                 torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        got = out.cpu().numpy().reshape(n, ivlen)
+        for i in list(range(0, n, 997)) + [n - 1]:
+            assert got[i].tobytes() == oracle_mod.ph_to_iv(int(seq[i]), int(flags[i]), ivlen), (ivlen, i)
+    out = torch.empty(65, dtype=torch.uint8, device=dev)
+    assert L.net2_ph_to_iv_dev(ds.data_ptr(), df.data_ptr(), 1, 65,
+                               out.data_ptr(), None) == 22  # EINVAL above 64
