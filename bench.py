@@ -35,8 +35,16 @@ CONFIGS = {
                workload="1M x mixed {64,512,1500} B packets, SHA-256, length-binned (configs[2])"),
     "c4": dict(alg=3, kind="fixed", n=1 << 20, length=1024,
                workload="1M x 1 KiB packets, SHA-512, device-resident (configs[3])"),
+    # SURVEY.md 8f rows, for DESIGN.md (not BASELINE configs)
+    "hmac": dict(alg=4, kind="fixed", n=1 << 20, length=1024,
+                 workload="1M x 1 KiB packets, HMAC-SHA256, device-resident (8f row 1)"),
+    "hmac_mtu": dict(alg=4, kind="mixed", n=1 << 20, length=None,
+                     workload="1M x mixed {64,512,1500} B datagrams, HMAC-SHA256, binned (8f row 1)"),
+    "ph_iv": dict(alg=1, kind="ph_iv", n=1 << 20, length=16,
+                  workload="1M packet headers -> 16-byte IVs, net2_ph_to_iv_dev (8f row 3)"),
 }
-DLEN = {1: 32, 2: 48, 3: 64}
+DLEN = {1: 32, 2: 48, 3: 64, 4: 32, 5: 48, 6: 64}
+HMAC_KEY = bytes(range(32))
 
 
 def dist_env():
@@ -55,6 +63,11 @@ def make_inputs(cfg, dev, seed):
         data = torch.randint(0, 256, (n * cfg["length"],), dtype=torch.uint8,
                              device=dev, generator=g)
         return dict(data=data, n=n, payload=n * cfg["length"])
+    if cfg["kind"] == "ph_iv":
+        seq = torch.arange(n, dtype=torch.int32, device=dev)
+        flags = torch.randint(0, 1 << 30, (n,), dtype=torch.int32, device=dev,
+                              generator=g)
+        return dict(seq=seq, flags=flags, n=n, payload=8 * n)
     choice = torch.tensor([64, 512, 1500], dtype=torch.int64, device=dev)
     lens = choice[torch.randint(0, 3, (n,), device=dev, generator=g)]
     offs = torch.zeros(n, dtype=torch.int64, device=dev)
@@ -141,12 +154,28 @@ def main():
     cfg = CONFIGS[args.config]
     inp = make_inputs(cfg, dev, seed=2 + rank)
     n, alg = inp["n"], cfg["alg"]
-    out = torch.empty((n, DLEN[alg]), dtype=torch.uint8, device=dev)
+    dlen = cfg["length"] if cfg["kind"] == "ph_iv" else DLEN[alg]
+    out = torch.empty((n, dlen), dtype=torch.uint8, device=dev)
     ws_buf = batch.var_workspace(n, dev) if cfg["kind"] == "mixed" else None
     stream = torch.cuda.current_stream(dev)
+    L = _lib.lib()
+    kbuf = HMAC_KEY[:DLEN[alg]] if alg >= 4 else b""
 
     def step():
-        if cfg["kind"] == "fixed":
+        if cfg["kind"] == "ph_iv":
+            _lib.check(L.net2_ph_to_iv_dev(inp["seq"].data_ptr(), inp["flags"].data_ptr(),
+                                           n, cfg["length"], out.data_ptr(),
+                                           stream.cuda_stream))
+        elif alg >= 4:
+            mixed = cfg["kind"] == "mixed"
+            _lib.check(L.net2_hmac_dev(
+                alg, kbuf, len(kbuf), inp["data"].data_ptr(),
+                inp["offs"].data_ptr() if mixed else None,
+                inp["lens"].data_ptr() if mixed else None,
+                cfg["length"] or 0, cfg["length"] or 0, n, out.data_ptr(),
+                ws_buf.data_ptr() if mixed and not args.unbinned else None,
+                ws_buf.numel() * 4 if mixed else 0, stream.cuda_stream))
+        elif cfg["kind"] == "fixed":
             batch.digest_fixed(alg, inp["data"], cfg["length"], cfg["length"],
                                n, out=out, stream=stream)
         else:
@@ -192,7 +221,7 @@ def main():
     # Roofline of the dominant kernel: algorithmic bytes = payload read +
     # digests written (+ 12 B/packet offsets+lens for the mixed layout),
     # per launch, over the event-timed launch duration.
-    per_launch = inp["payload"] + n * DLEN[alg] + (12 * n if cfg["kind"] == "mixed" else 0)
+    per_launch = inp["payload"] + n * dlen + (12 * n if cfg["kind"] == "mixed" else 0)
     achieved = per_launch / (launch_ms / 1e3) / 1e9
     pmc = load_pmc(args.config)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -220,22 +249,24 @@ def main():
 
     line = {
         "metric": METRIC if args.config == "c2" else
-        f"{'SHA-512' if alg == 3 else 'SHA-256'} digests/s, {cfg['workload']}",
+        f"{'SHA-512' if alg == 3 else 'SHA-256'} {'IVs' if cfg['kind'] == 'ph_iv' else 'digests'}/s, {cfg['workload']}",
         "value": round(value, 1), "unit": "digests/s", "n_gpus": ws,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "prewarm_ms": args.prewarm_ms,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u32" if alg == 1 else "u64",
+        "scaling": "weak", "vs_baseline": None, "dtype": "u64" if alg in (2, 3, 5, 6) else "u32",
         "data": "synthetic: uniform random bytes (torch.randint, seed 2+rank), resident in HBM before timing",
         "config": {"workload": cfg["workload"] + (" [unbinned]" if args.unbinned else ""),
-                   "packets_per_gpu": n, "alg": "SHA256" if alg == 1 else "SHA512",
+                   "packets_per_gpu": n,
+                   "alg": {1: "SHA256", 2: "SHA384", 3: "SHA512", 4: "HMAC-SHA256",
+                           5: "HMAC-SHA384", 6: "HMAC-SHA512"}[alg],
                    "payload_bytes_per_gpu": inp["payload"],
                    "parallelism": f"{ws} independent shards, no collective"},
         "roofline": roof,
     }
     if valu:
         line["roofline_valu"] = valu
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline and args.config in ("c2", "c3", "c4"):
         line["cpu_baseline"] = cpu_baseline(cfg)
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -1,0 +1,110 @@
+#!/usr/bin/env python3
+"""BASELINE config 1 shape through the signed-payload path: 4096 x 1 KiB
+payloads, hash-then-sign (types/signature.n2t:60-119) and validate
+(:124-175) with the P-521 key of test/sign.c:27-45.
+
+Reports, per stage: the GPU batch digest (net2_sha2_batch, host memory in
+and out), ECDSA over the digests on host threads, and the batched
+net2_signature_create_batch / _validate_batch end to end; plus the same flow
+with the oracle's CPU digests (the reference's per-payload SHA512 on one
+core, test/sign.c's shape) as the baseline.  One JSON line per measurement.
+"""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+class Sig(ctypes.Structure):
+    _fields_ = [("sign_alg", ctypes.c_char_p), ("hash_alg", ctypes.c_char_p),
+                ("data", ctypes.c_void_p), ("datalen", ctypes.c_size_t)]
+
+
+def main():
+    import ilias_net2_amd._lib as L
+    from oracle import oracle
+    import synth
+    L.lib()
+    S = ctypes.CDLL(os.path.join(ROOT, "ilias_net2_amd", "libnet2_sign.so"))
+    S.net2_signctx_privnew.restype = ctypes.c_void_p
+    S.net2_signctx_pubnew.restype = ctypes.c_void_p
+    S.net2_signctx_maxmsglen.restype = ctypes.c_size_t
+    S.net2_signctx_maxmsglen.argtypes = [ctypes.c_void_p]
+    S.net2_signature_deinit.restype = None
+    keys = [open(os.path.join(ROOT, "tests", "golden", "keys", f), "rb").read()
+            for f in ("ecdsa_p521_priv.pem", "ecdsa_p521_pub.pem")]
+    priv = ctypes.c_void_p(S.net2_signctx_privnew(0, keys[0], len(keys[0])))
+    pub = ctypes.c_void_p(S.net2_signctx_pubnew(0, keys[1], len(keys[1])))
+    assert priv and pub
+    n, length = 4096, 1024
+    threads = min(16, len(os.sched_getaffinity(0)))
+    data = synth.fixed_batch(1, n, length)
+    offs = (np.arange(n, dtype=np.uint64) * length)
+    lens = np.full(n, length, dtype=np.uint32)
+    ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    res = []
+
+    def timeit(fn, reps=3):
+        fn()
+        best = 1e9
+        for _ in range(reps):
+            t = time.perf_counter()
+            fn()
+            best = min(best, time.perf_counter() - t)
+        return best
+
+    for alg, name in ((3, "SHA512"), (1, "SHA256")):
+        dig = np.empty((n, 64 if alg == 3 else 32), dtype=np.uint8)
+        t = timeit(lambda: L.check(L.lib().net2_sha2_batch(
+            alg, ptr(data), ptr(offs), ptr(lens), 0, 0, n, ptr(dig), 1)))
+        res.append({"stage": f"GPU digest {name} (net2_sha2_batch, host mem, 1 GPU)",
+                    "payloads_per_s": n / t, "ms": t * 1e3})
+        t = timeit(lambda: oracle.batch(alg, data, stride=length, length=length,
+                                        n=n, nthreads=1))
+        res.append({"stage": f"CPU digest {name} (oracle, 1 core = test/sign.c shape)",
+                    "payloads_per_s": n / t, "ms": t * 1e3})
+    sigs = (Sig * n)()
+    valid = (ctypes.c_int * n)()
+
+    def create():
+        rc = S.net2_signature_create_batch(sigs, ptr(data), ptr(offs), ptr(lens),
+                                           ctypes.c_size_t(n), 3, priv, threads)
+        assert rc == 0, rc
+
+    def validate():
+        rc = S.net2_signature_validate_batch(sigs, ptr(data), ptr(offs), ptr(lens),
+                                             ctypes.c_size_t(n), pub, valid, threads)
+        assert rc == 0, rc
+
+    def free_all():
+        for i in range(n):
+            S.net2_signature_deinit(ctypes.byref(sigs[i]))
+
+    create()
+    t_c = 1e9
+    for _ in range(2):
+        free_all()
+        t0 = time.perf_counter()
+        create()
+        t_c = min(t_c, time.perf_counter() - t0)
+    t_v = timeit(validate, reps=2)
+    assert all(v == 1 for v in valid)
+    res.append({"stage": f"net2_signature_create_batch SHA512+ECDSA-P521, {threads} threads",
+                "payloads_per_s": n / t_c, "ms": t_c * 1e3})
+    res.append({"stage": f"net2_signature_validate_batch SHA512+ECDSA-P521, {threads} threads",
+                "payloads_per_s": n / t_v, "ms": t_v * 1e3})
+    free_all()
+    for r in res:
+        r["config"] = "4096 x 1 KiB payloads (BASELINE configs[0] shape)"
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
