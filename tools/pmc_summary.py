@@ -21,7 +21,6 @@ from __future__ import annotations
 
 import argparse
 import csv
-import glob
 import json
 import os
 import shutil
@@ -59,7 +58,12 @@ def main():
     pat = KERNEL[args.cfg]
 
     counters, durs_all = {}, []
-    for path in sorted(glob.glob(os.path.join(args.src, f"pmc_{args.cfg}_*", "run_counter_collection.csv"))):
+    tags = ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "FETCH_SIZE", "WRITE_SIZE",
+            "SQ_INSTS_SALU")
+    for tag in tags:
+        path = os.path.join(args.src, f"pmc_{args.cfg}_{tag}", "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
         c, d = per_dispatch(path, pat)
         for k, v in c.items():
             counters[k] = v
