@@ -131,6 +131,7 @@ def main():
                          "the first ~50 launches ~15%% slower)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS) + ["e2e"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--unbinned", action="store_true",
                     help="c3: hash in submission order (ablation)")
     args = ap.parse_args()
@@ -140,11 +141,17 @@ def main():
     from ilias_net2_amd import batch, _lib
 
     ws, rank, local = dist_env()
-    if ws > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if ws > 1 else 0)
+    # One process per GPU.  --dist-backend gloo with more ranks than GPUs
+    # (device = local rank mod device count) rehearses the N>1 path on a
+    # 1-GPU box; the driver's multi-GPU runs use RCCL ("nccl").
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", (local % ndev) if ws > 1 else 0)
     torch.cuda.set_device(dev)
+    if ws > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
     if _lib.device_count() < 1:
         raise SystemExit("no gfx950 device visible to libnet2_sha2.so")
 
@@ -210,7 +217,8 @@ def main():
     launch_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
 
     if ws > 1:
-        t = torch.tensor([elapsed, launch_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, launch_ms], dtype=torch.float64,
+                         device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, launch_ms = float(t[0]), float(t[1])
 
@@ -300,7 +308,8 @@ def run_e2e(args, ws, rank, dev):
         dist.barrier()
     el = time.perf_counter() - t0
     if ws > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64,
+                         device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t[0])
     ms = el * 1e3 / args.steps
