@@ -300,13 +300,29 @@ __device__ __forceinline__ uint64_t bsig1_512(uint64_t e)
 {
 	return xor3_64(ror64<14>(e), ror64<18>(e), ror64<41>(e));
 }
+/*
+ * 64-bit logical shift as one v_lshrrev_b64 (hipcc otherwise emits
+ * v_alignbit_b32 + v_lshrrev_b32, two VALU ops for the same result).
+ */
+template <int N>
+__device__ __forceinline__ uint64_t shr64(uint64_t x)
+{
+#ifdef NET2_SHR64_ASM
+	uint64_t r;
+	asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(N), "v"(x));
+	return r;
+#else
+	return x >> N;
+#endif
+}
+
 __device__ __forceinline__ uint64_t ssig0_512(uint64_t x)
 {
-	return xor3_64(ror64<1>(x), ror64<8>(x), x >> 7);
+	return xor3_64(ror64<1>(x), ror64<8>(x), shr64<7>(x));
 }
 __device__ __forceinline__ uint64_t ssig1_512(uint64_t x)
 {
-	return xor3_64(ror64<19>(x), ror64<61>(x), x >> 6);
+	return xor3_64(ror64<19>(x), ror64<61>(x), shr64<6>(x));
 }
 
 template <int T>

@@ -103,12 +103,14 @@ struct Sha512 {
 
 /*
  * Address modes.  A16: every packet start in the wave is 16-byte aligned, a
- * block is NW32/4 global_load_dwordx4.  A1: arbitrary byte alignment; the
+ * block is NW32/4 global_load_dwordx4.  A4: dword-aligned starts (packed
+ * packets whose lengths are multiples of 4, e.g. 1,500-byte datagrams), a
+ * block is NW32 global_load_dword.  A1: arbitrary byte alignment; the
  * block is read as NW32 + 1 naturally aligned dwords (the extra one only
  * when misaligned, so no dword outside the packet's own bytes is touched)
  * and re-aligned with v_alignbyte_b32.
  */
-enum { AMODE_A16 = 0, AMODE_A1 = 1 };
+enum { AMODE_A16 = 0, AMODE_A1 = 1, AMODE_A4 = 2 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -130,6 +132,11 @@ __device__ __forceinline__ void issue_block(const uint8_t *p, Raw<NW32> &r)
 			r.d[4 * i + 2] = v.z;
 			r.d[4 * i + 3] = v.w;
 		}
+	} else if (AMODE == AMODE_A4) {
+		const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
+#pragma unroll
+		for (int i = 0; i < NW32; i++)
+			r.d[i] = q[i];
 	} else {
 		uintptr_t a = reinterpret_cast<uintptr_t>(p);
 		const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
@@ -145,7 +152,7 @@ template <int NW32, int AMODE>
 __device__ __forceinline__ void finish_block(const uint8_t *p,
     const Raw<NW32> &r, uint32_t (&w)[NW32])
 {
-	if (AMODE == AMODE_A16) {
+	if (AMODE == AMODE_A16 || AMODE == AMODE_A4) {
 #pragma unroll
 		for (int i = 0; i < NW32; i++)
 			w[i] = bswap32(r.d[i]);
@@ -368,6 +375,8 @@ __global__ __launch_bounds__(256) void var_kernel(const uint8_t *__restrict__ ba
 
 	if (__all((reinterpret_cast<uintptr_t>(p) & 15) == 0))
 		digest_one<H, AMODE_A16, false>(p, len, is384, nullptr, st);
+	else if (__all((reinterpret_cast<uintptr_t>(p) & 3) == 0))
+		digest_one<H, AMODE_A4, false>(p, len, is384, nullptr, st);
 	else
 		digest_one<H, AMODE_A1, false>(p, len, is384, nullptr, st);
 	if (!live)
@@ -581,6 +590,40 @@ __device__ __forceinline__ uint32_t bin_of(uint32_t len, int blk_shift,
 	return nbins - 1 - b;	/* descending block count */
 }
 
+/* Packets per thread in the binning kernels: one workgroup bins a tile of
+ * 256 x 16 = 4,096 packets, so the 2,048-entry LDS histogram is cleared
+ * and flushed once per 4,096 packets. */
+#define NET2_BIN_ITEMS 16
+#define NET2_BIN_TILE (256 * NET2_BIN_ITEMS)
+
+/*
+ * Wave-aggregated LDS counter add: the lanes of a wave that carry the same
+ * key elect one leader that adds the group's size once (a {64,512,1500}
+ * batch puts 3 keys in a wave: 3 LDS atomics instead of 64).  Returns the
+ * counter's value before the group's add plus this lane's rank in its group.
+ */
+__device__ __forceinline__ uint32_t wave_rank_add(uint32_t *ctr, uint32_t key,
+    bool active)
+{
+	uint64_t todo = __ballot(active);
+	const uint64_t below = __lanemask_lt();
+	const int lane = (int)__lane_id();
+	uint32_t rank = 0;
+	while (todo != 0) {
+		const int leader = __ffsll((unsigned long long)todo) - 1;
+		const uint32_t k = __shfl(key, leader);
+		const uint64_t grp = __ballot(active && key == k);
+		uint32_t base = 0;
+		if (lane == leader)
+			base = atomicAdd(&ctr[k], (uint32_t)__popcll(grp));
+		base = __shfl(base, leader);
+		if (active && key == k)
+			rank = base + (uint32_t)__popcll(grp & below);
+		todo &= ~grp;
+	}
+	return rank;
+}
+
 __global__ __launch_bounds__(256) void bin_count_kernel(
     const uint32_t *__restrict__ lens, uint64_t n, int blk_shift,
     int lenbytes, uint32_t *__restrict__ hist)
@@ -589,11 +632,15 @@ __global__ __launch_bounds__(256) void bin_count_kernel(
 	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
 		lh[b] = 0;
 	__syncthreads();
-	const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-	for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-	    i += stride)
-		atomicAdd(&lh[bin_of(lens[i], blk_shift, lenbytes,
-		    NET2_SHA2_NBINS)], 1u);
+	const uint64_t i0 = (uint64_t)blockIdx.x * NET2_BIN_TILE + threadIdx.x;
+#pragma unroll
+	for (int k = 0; k < NET2_BIN_ITEMS; k++) {
+		const uint64_t i = i0 + (uint64_t)k * 256;
+		const bool live = i < n;
+		const uint32_t bin = live ? bin_of(lens[i], blk_shift, lenbytes,
+		    NET2_SHA2_NBINS) : 0;
+		(void)wave_rank_add(lh, bin, live);
+	}
 	__syncthreads();
 	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
 		if (lh[b] != 0)
@@ -638,27 +685,29 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(
 {
 	__shared__ uint32_t cnt[NET2_SHA2_NBINS];
 	__shared__ uint32_t basep[NET2_SHA2_NBINS];
-	const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-	for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n;
-	    i0 += stride) {
-		for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
-			cnt[b] = 0;
-		__syncthreads();
-		const uint64_t i = i0 + threadIdx.x;
-		uint32_t bin = 0, rank = 0;
-		if (i < n) {
-			bin = bin_of(lens[i], blk_shift, lenbytes,
-			    NET2_SHA2_NBINS);
-			rank = atomicAdd(&cnt[bin], 1u);
-		}
-		__syncthreads();
-		for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
-			if (cnt[b] != 0)
-				basep[b] = atomicAdd(&cursor[b], cnt[b]);
-		__syncthreads();
+	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
+		cnt[b] = 0;
+	__syncthreads();
+	const uint64_t i0 = (uint64_t)blockIdx.x * NET2_BIN_TILE + threadIdx.x;
+	uint32_t bin[NET2_BIN_ITEMS], rank[NET2_BIN_ITEMS];
+#pragma unroll
+	for (int k = 0; k < NET2_BIN_ITEMS; k++) {
+		const uint64_t i = i0 + (uint64_t)k * 256;
+		const bool live = i < n;
+		bin[k] = live ? bin_of(lens[i], blk_shift, lenbytes,
+		    NET2_SHA2_NBINS) : 0;
+		rank[k] = wave_rank_add(cnt, bin[k], live);
+	}
+	__syncthreads();
+	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
+		if (cnt[b] != 0)
+			basep[b] = atomicAdd(&cursor[b], cnt[b]);
+	__syncthreads();
+#pragma unroll
+	for (int k = 0; k < NET2_BIN_ITEMS; k++) {
+		const uint64_t i = i0 + (uint64_t)k * 256;
 		if (i < n)
-			perm[basep[bin] + rank] = (uint32_t)i;
-		__syncthreads();
+			perm[basep[bin[k]] + rank[k]] = (uint32_t)i;
 	}
 }
 
@@ -775,9 +824,7 @@ hipError_t net2_bin_order(int alg, const uint32_t *lens, uint64_t n,
 	    s);
 	if (e != hipSuccess)
 		return e;
-	unsigned g = grid_for(n);
-	if (g > 2048)
-		g = 2048;
+	const unsigned g = (unsigned)((n + NET2_BIN_TILE - 1) / NET2_BIN_TILE);
 	bin_count_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift, lenbytes, hist);
 	bin_scan_kernel<<<1, 1024, 0, s>>>(hist, cursor);
 	bin_scatter_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift, lenbytes, cursor,
