@@ -18,6 +18,17 @@ from . import _lib
 from ._lib import DIGEST_LEN, check
 
 
+def _need(t, dtype, what: str):
+    """Device tensors are passed as raw pointers: check what the C ABI
+    assumes (dtype, contiguity, a GPU device) before handing them over."""
+    if t.dtype != dtype:
+        raise TypeError(f"{what} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{what} must be contiguous")
+    if t.device.type != "cuda":
+        raise ValueError(f"{what} must live on the GPU")
+
+
 def _stream_ptr(stream) -> Optional[int]:
     if stream is None:
         import torch
@@ -35,8 +46,12 @@ def digest_fixed(alg: int, data, stride: int, length: int, n: int, out=None,
     ``stream`` (default: torch's current stream)."""
     import torch
     dl = DIGEST_LEN[alg]
+    _need(data, torch.uint8, "data")
     if out is None:
         out = torch.empty((n, dl), dtype=torch.uint8, device=data.device)
+    _need(out, torch.uint8, "out")
+    if out.numel() < n * dl:
+        raise ValueError("out too small")
     if n and data.numel() < (n - 1) * stride + length:
         raise ValueError("data tensor too small for n packets")
     rc = _lib.lib().net2_sha2_dev_fixed(alg, data.data_ptr(), stride, length,
@@ -60,8 +75,16 @@ def digest_var(alg: int, data, offsets, lens, out=None, workspace=None,
     import torch
     n = int(offsets.numel())
     dl = DIGEST_LEN[alg]
+    _need(data, torch.uint8, "data")
+    _need(offsets, torch.int64, "offsets")
+    _need(lens, torch.int32, "lens")
+    if lens.numel() != n:
+        raise ValueError("offsets and lens differ in length")
     if out is None:
         out = torch.empty((n, dl), dtype=torch.uint8, device=data.device)
+    _need(out, torch.uint8, "out")
+    if out.numel() < n * dl:
+        raise ValueError("out too small")
     ws_ptr, ws_bytes = None, 0
     if binned and n:
         if workspace is None:
@@ -105,7 +128,10 @@ def hmac_dev(alg: int, key: bytes, data, stride: int = 0, length: int = 0,
     key: fixed layout (stride/length/n) or variable layout (offsets/lens)."""
     import torch
     dl = DIGEST_LEN[alg]
+    _need(data, torch.uint8, "data")
     if offsets is not None:
+        _need(offsets, torch.int64, "offsets")
+        _need(lens, torch.int32, "lens")
         n = int(offsets.numel())
     if out is None:
         out = torch.empty((n, dl), dtype=torch.uint8, device=data.device)

@@ -356,3 +356,65 @@ def test_ph_to_iv(dev, oracle_mod):
     out = torch.empty(65, dtype=torch.uint8, device=dev)
     assert L.net2_ph_to_iv_dev(ds.data_ptr(), df.data_ptr(), 1, 65,
                                out.data_ptr(), None) == 22  # EINVAL above 64
+
+
+# ---- host threading and graph capture (include/net2/sha2_batch.h) -------------
+
+def test_concurrent_host_threads(dev, H, oracle_mod):
+    """Callers are threadpool workers in the reference (threadpool.h:33-34):
+    many threads calling hashbuf / net2_sha2_batch at once."""
+    import threading
+    from ilias_net2_amd import batch
+    errors = []
+
+    def worker(t):
+        try:
+            rng = np.random.default_rng(t)
+            for j in range(20):
+                m = rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()
+                alg = 1 + (t + j) % 3
+                if H.hashbuf(alg, b"", m) != oracle_mod.digest(alg, m):
+                    errors.append(("hashbuf", t, j))
+            data = synth.fixed_batch(500 + t, 3000, 700)
+            got = batch.digest_host(1 + t % 3, data, stride=700, length=700, n=3000)
+            if not np.array_equal(got, oracle_mod.batch(1 + t % 3, data, stride=700,
+                                                        length=700, n=3000)):
+                errors.append(("batch", t))
+        except Exception as e:  # noqa: BLE001
+            errors.append(("exc", t, repr(e)))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errors, errors[:5]
+
+
+def test_graph_capture(dev, batch, oracle_mod):
+    """The device entry points allocate and synchronise nothing, so a batch
+    launch can be captured into a hipGraph and replayed."""
+    n, length = 5000, 1024
+    data = to_dev(synth.fixed_batch(77, n, length), dev)
+    lens = synth.mixed_lengths(78, n)
+    vdata, offs = synth.packed(79, lens)
+    vd, vo, vl = to_dev(vdata, dev), to_dev(offs.astype(np.int64), dev), to_dev(lens.astype(np.int32), dev)
+    out = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
+    vout = torch.zeros((n, 64), dtype=torch.uint8, device=dev)
+    ws = batch.var_workspace(n, dev)
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):  # warm-up outside capture
+        batch.digest_fixed(1, data, length, length, n, out=out, stream=s)
+        batch.digest_var(3, vd, vo, vl, out=vout, workspace=ws, stream=s)
+    torch.cuda.synchronize()
+    out.zero_()
+    vout.zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        batch.digest_fixed(1, data, length, length, n, out=out, stream=s)
+        batch.digest_var(3, vd, vo, vl, out=vout, workspace=ws, stream=s)
+    g.replay()
+    torch.cuda.synchronize()
+    want = oracle_mod.batch(1, data.cpu().numpy(), stride=length, length=length, n=n)
+    assert np.array_equal(out.cpu().numpy(), want)
+    assert np.array_equal(vout.cpu().numpy(), oracle_mod.batch(3, vdata, offsets=offs, lens=lens))
