@@ -79,6 +79,17 @@ def make_inputs(cfg, dev, seed):
                 payload=total)
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(cfg):
     """Oracle (clean-room C restatement of src/sha2.c, -O3) on host cores."""
     import numpy as np
@@ -103,7 +114,19 @@ def cpu_baseline(cfg):
         t0 = time.perf_counter()
         run(threads)
         best = min(best, time.perf_counter() - t0)
+    # also one thread, on the first n/16 packets (same shape)
+    n1 = max(1, n // 16)
+    if cfg["kind"] == "fixed":
+        one = lambda: oracle.batch(alg, data, stride=cfg["length"],  # noqa: E731
+                                   length=cfg["length"], n=n1, nthreads=1)
+    else:
+        one = lambda: oracle.batch(alg, data, offsets=offs[:n1], lens=lens[:n1],  # noqa: E731
+                                   nthreads=1)
+    t0 = time.perf_counter()
+    one()
+    single = n1 / (time.perf_counter() - t0)
     return {"value": n / best, "unit": "digests/s", "cores": threads,
+            "single_thread_value": single, "cpu_model": _cpu_model(),
             "kind": "port",
             "sample": (f"the full {cfg['workload'].split(' packets')[0]} packet batch from host memory, "
                        f"oracle/sha2_oracle.c (-O3, rolled transform like src/sha2.c:374-445) "

@@ -122,65 +122,67 @@ static inline uint64_t ror64(uint64_t x, unsigned n)
 
 /* ---- compression functions (FIPS 180-4 6.2.2 / 6.4.2) ------------------ */
 
+/*
+ * One round over message word x (FIPS 180-4 6.2.2 step 3 / 6.4.2 step 3);
+ * the working variables rotate by renaming, as src/sha2.c's ROUND256 /
+ * ROUND512 macros do.
+ */
+#define ORACLE_ROUND(T, S1, S0, kt, x) do {				\
+	T t1_ = h + S1(e) + ((e & f) ^ (~e & g)) + (kt) + (x);		\
+	T t2_ = S0(a) + ((a & b) ^ (a & c) ^ (b & c));			\
+	h = g; g = f; f = e; e = d + t1_;				\
+	d = c; c = b; b = a; a = t1_ + t2_;				\
+} while (0)
+
+#define BIG0_256(x) (ror32(x, 2) ^ ror32(x, 13) ^ ror32(x, 22))
+#define BIG1_256(x) (ror32(x, 6) ^ ror32(x, 11) ^ ror32(x, 25))
+#define SML0_256(x) (ror32(x, 7) ^ ror32(x, 18) ^ ((x) >> 3))
+#define SML1_256(x) (ror32(x, 17) ^ ror32(x, 19) ^ ((x) >> 10))
+#define BIG0_512(x) (ror64(x, 28) ^ ror64(x, 34) ^ ror64(x, 39))
+#define BIG1_512(x) (ror64(x, 14) ^ ror64(x, 18) ^ ror64(x, 41))
+#define SML0_512(x) (ror64(x, 1) ^ ror64(x, 8) ^ ((x) >> 7))
+#define SML1_512(x) (ror64(x, 19) ^ ror64(x, 61) ^ ((x) >> 6))
+
 void oracle_sha256_transform(uint32_t st[8], const uint8_t blk[64])
 {
-	uint32_t w[64], v[8];
+	/* 16-word circular schedule (src/sha2.c:374-445, rolled form). */
+	uint32_t w[16];
+	uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+	uint32_t e = st[4], f = st[5], g = st[6], h = st[7];
 	int t;
 
-	for (t = 0; t < 16; t++)
+	for (t = 0; t < 16; t++) {
 		w[t] = load_be32(blk + 4 * t);
-	for (t = 16; t < 64; t++) {
-		uint32_t s0 = ror32(w[t - 15], 7) ^ ror32(w[t - 15], 18) ^
-		    (w[t - 15] >> 3);
-		uint32_t s1 = ror32(w[t - 2], 17) ^ ror32(w[t - 2], 19) ^
-		    (w[t - 2] >> 10);
-		w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+		ORACLE_ROUND(uint32_t, BIG1_256, BIG0_256, k32[t], w[t]);
 	}
-	memcpy(v, st, sizeof(v));
-	for (t = 0; t < 64; t++) {
-		/* v[0..7] = a..h */
-		uint32_t e = v[4], a = v[0];
-		uint32_t big1 = ror32(e, 6) ^ ror32(e, 11) ^ ror32(e, 25);
-		uint32_t ch = (e & v[5]) ^ (~e & v[6]);
-		uint32_t t1 = v[7] + big1 + ch + k32[t] + w[t];
-		uint32_t big0 = ror32(a, 2) ^ ror32(a, 13) ^ ror32(a, 22);
-		uint32_t maj = (a & v[1]) ^ (a & v[2]) ^ (v[1] & v[2]);
-		memmove(v + 1, v, 7 * sizeof(v[0]));
-		v[4] += t1;
-		v[0] = t1 + big0 + maj;
+	for (; t < 64; t++) {
+		uint32_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
+		w[t & 15] += SML0_256(w15) + w[(t + 9) & 15] + SML1_256(w2);
+		ORACLE_ROUND(uint32_t, BIG1_256, BIG0_256, k32[t], w[t & 15]);
 	}
-	for (t = 0; t < 8; t++)
-		st[t] += v[t];
+	st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+	st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
 void oracle_sha512_transform(uint64_t st[8], const uint8_t blk[128])
 {
-	uint64_t w[80], v[8];
+	/* src/sha2.c:663-734, same structure as the SHA-256 one above. */
+	uint64_t w[16];
+	uint64_t a = st[0], b = st[1], c = st[2], d = st[3];
+	uint64_t e = st[4], f = st[5], g = st[6], h = st[7];
 	int t;
 
-	for (t = 0; t < 16; t++)
+	for (t = 0; t < 16; t++) {
 		w[t] = load_be64(blk + 8 * t);
-	for (t = 16; t < 80; t++) {
-		uint64_t s0 = ror64(w[t - 15], 1) ^ ror64(w[t - 15], 8) ^
-		    (w[t - 15] >> 7);
-		uint64_t s1 = ror64(w[t - 2], 19) ^ ror64(w[t - 2], 61) ^
-		    (w[t - 2] >> 6);
-		w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+		ORACLE_ROUND(uint64_t, BIG1_512, BIG0_512, k64[t], w[t]);
 	}
-	memcpy(v, st, sizeof(v));
-	for (t = 0; t < 80; t++) {
-		uint64_t e = v[4], a = v[0];
-		uint64_t big1 = ror64(e, 14) ^ ror64(e, 18) ^ ror64(e, 41);
-		uint64_t ch = (e & v[5]) ^ (~e & v[6]);
-		uint64_t t1 = v[7] + big1 + ch + k64[t] + w[t];
-		uint64_t big0 = ror64(a, 28) ^ ror64(a, 34) ^ ror64(a, 39);
-		uint64_t maj = (a & v[1]) ^ (a & v[2]) ^ (v[1] & v[2]);
-		memmove(v + 1, v, 7 * sizeof(v[0]));
-		v[4] += t1;
-		v[0] = t1 + big0 + maj;
+	for (; t < 80; t++) {
+		uint64_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
+		w[t & 15] += SML0_512(w15) + w[(t + 9) & 15] + SML1_512(w2);
+		ORACLE_ROUND(uint64_t, BIG1_512, BIG0_512, k64[t], w[t & 15]);
 	}
-	for (t = 0; t < 8; t++)
-		st[t] += v[t];
+	st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+	st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
 /* ---- SHA-256 streaming API ---------------------------------------------- */

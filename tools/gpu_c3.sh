@@ -12,5 +12,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run 
 AB512=1 timeout -k 10 200 ./tools/kernel_ab > gpurun_out/ab512_base.json 2>&1 || exit $?
 AB512=1 timeout -k 10 200 ./tools/kernel_ab_shr > gpurun_out/ab512_shr.json 2>&1 || exit $?
 AB512=1 timeout -k 10 200 ./tools/kernel_ab > gpurun_out/ab512_base2.json 2>&1 || exit $?
+timeout -k 10 200 ./tools/kernel_ab > gpurun_out/ab256.json 2>&1 || exit $?
+cat gpurun_out/ab256.json
 grep S0 gpurun_out/ab512_base.json gpurun_out/ab512_shr.json gpurun_out/ab512_base2.json
 exit 0

@@ -44,6 +44,67 @@ void k_stride(const uint8_t *base, uint32_t len, uint64_t n, uint8_t *out, KW pa
 		fixed_lane<Sha256, AMODE_A16, true>(i, base, len, len, out, 32, 0, pad.kw);
 }
 
+/*
+ * LDS-staged variant (the north-star's "blocks coalesced from HBM into an
+ * LDS-staged schedule"): each wave owns a 4 KiB LDS slab holding block k of
+ * its 64 packets.  Block k+1 is fetched with 4 global_load_lds_dwordx4 per
+ * wave -- 16 packets x 64 B per instruction, 4 lanes per packet, so each
+ * instruction touches 16 whole 64-B segments instead of 64 scattered
+ * 16-B pieces -- while block k (already copied LDS -> VGPR) is compressed.
+ * The LDS image is lane-linear; the chunk order inside a packet is XOR-
+ * swizzled on the global side (c ^ (p>>2 & 3)) so that the per-lane
+ * ds_read_b128 of a 64-B row is bank-conflict free.  Requires n % 64 == 0,
+ * stride % 16 == 0, len % 64 == 0.
+ */
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+__global__ __launch_bounds__(256) void k_lds(const uint8_t *base, uint32_t len,
+    uint64_t n, uint8_t *out, KW pad)
+{
+	__shared__ u32x4 slab[4][256];
+	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+	const uint64_t w0 = (uint64_t)blockIdx.x * 256 + wv * 64;
+	const uint32_t nfull = len / 64;
+	u32x4 *my = slab[wv];
+
+	/* loader geometry: instruction j, lane l -> packet 16j + l/4 */
+	auto issue = [&](uint32_t k) {
+#pragma unroll
+		for (int j = 0; j < 4; j++) {
+			const int p = 16 * j + (lane >> 2);
+			const int c = (lane & 3) ^ ((p >> 2) & 3);
+			const uint8_t *g = base + (w0 + p) * (uint64_t)len + k * 64 + c * 16;
+			__builtin_amdgcn_global_load_lds((glb_void *)g,
+			    (lds_void *)(my + 64 * j), 16, 0, 0);
+		}
+	};
+	uint32_t st[8];
+	Sha256::init(st, 0);
+	issue(0);
+	const int f = (lane >> 2) & 3;
+	for (uint32_t k = 0; k < nfull; k++) {
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		uint32_t w[16];
+#pragma unroll
+		for (int c = 0; c < 4; c++) {
+			u32x4 v = my[4 * lane + (c ^ f)];
+			w[4 * c] = bswap32(v.x);
+			w[4 * c + 1] = bswap32(v.y);
+			w[4 * c + 2] = bswap32(v.z);
+			w[4 * c + 3] = bswap32(v.w);
+		}
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+		if (k + 1 < nfull)
+			issue(k + 1);
+		compress256(st, w);
+	}
+	compress256_kw(st, pad.kw);
+	uint32_t o[16];
+	Sha256::out_words(st, o, 0);
+	store_digest<32>(out + (w0 + lane) * 32, o);
+}
+
 typedef PadKW<uint64_t> KW5;
 
 template <int AM, bool PF>
@@ -128,6 +189,7 @@ int main()
 		{"E block64 sgpr80", [&](uint8_t *o) { k_sgpr80<64><<<n / 64, 64>>>(d_in, len, n, o, pad); }},
 		{"F stride 256x(8/CU) sgpr80", [&](uint8_t *o) { k_stride<256><<<cus * 8, 256>>>(d_in, len, n, o, pad); }},
 		{"G stride 64x(32/CU) sgpr80", [&](uint8_t *o) { k_stride<64><<<cus * 32, 64>>>(d_in, len, n, o, pad); }},
+		{"L block256 LDS-staged glds", [&](uint8_t *o) { k_lds<<<n / 256, 256>>>(d_in, len, n, o, pad); }},
 	};
 	if (do512)
 		vs = vs512;
