@@ -40,11 +40,19 @@ CONFIGS = {
                  workload="1M x 1 KiB packets, HMAC-SHA256, device-resident (8f row 1)"),
     "hmac_mtu": dict(alg=4, kind="mixed", n=1 << 20, length=None,
                      workload="1M x mixed {64,512,1500} B datagrams, HMAC-SHA256, binned (8f row 1)"),
+    # HMAC-SHA512 is what select_hash (conn_negotiator.c:110-131) picks when
+    # every registry row is offered: the default per-datagram authenticator
+    "hmac512": dict(alg=6, kind="fixed", n=1 << 20, length=1024,
+                    workload="1M x 1 KiB packets, HMAC-SHA512, device-resident (8f row 1)"),
+    "hmac512_mtu": dict(alg=6, kind="mixed", n=1 << 20, length=None,
+                        workload="1M x mixed {64,512,1500} B datagrams, HMAC-SHA512, binned (8f row 1)"),
     "ph_iv": dict(alg=1, kind="ph_iv", n=1 << 20, length=16,
                   workload="1M packet headers -> 16-byte IVs, net2_ph_to_iv_dev (8f row 3)"),
 }
 DLEN = {1: 32, 2: 48, 3: 64, 4: 32, 5: 48, 6: 64}
-HMAC_KEY = bytes(range(32))
+ALG_NAMES = {1: "SHA-256", 2: "SHA-384", 3: "SHA-512", 4: "HMAC-SHA256",
+             5: "HMAC-SHA384", 6: "HMAC-SHA512"}
+HMAC_KEY = bytes(range(64))
 
 
 def dist_env():
@@ -280,7 +288,8 @@ def main():
 
     line = {
         "metric": METRIC if args.config == "c2" else
-        f"{'SHA-512' if alg == 3 else 'SHA-256'} {'IVs' if cfg['kind'] == 'ph_iv' else 'digests'}/s, {cfg['workload']}",
+        ("SHA-256 IVs/s, " if cfg["kind"] == "ph_iv" else
+         f"{ALG_NAMES[alg]} digests/s, ") + cfg["workload"],
         "value": round(value, 1), "unit": "digests/s", "n_gpus": ws,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
@@ -289,8 +298,7 @@ def main():
         "data": "synthetic: uniform random bytes (torch.randint, seed 2+rank), resident in HBM before timing",
         "config": {"workload": cfg["workload"] + (" [unbinned]" if args.unbinned else ""),
                    "packets_per_gpu": n,
-                   "alg": {1: "SHA256", 2: "SHA384", 3: "SHA512", 4: "HMAC-SHA256",
-                           5: "HMAC-SHA384", 6: "HMAC-SHA512"}[alg],
+                   "alg": ALG_NAMES[alg].replace("-", "") if alg <= 3 else ALG_NAMES[alg],
                    "payload_bytes_per_gpu": inp["payload"],
                    "parallelism": f"{ws} independent shards, no collective"},
         "roofline": roof,

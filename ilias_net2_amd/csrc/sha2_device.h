@@ -353,11 +353,21 @@ __device__ __forceinline__ uint64_t expand512(uint64_t (&w)[16])
  *      k512_lds_fill() at kernel entry), read with one broadcast
  *      ds_read_b64 per round: the constant costs an LDS issue slot instead of
  *      VALU time or SGPRs.  The read is volatile so it is not hoisted out of
- *      the block loop (which would pin 160 VGPRs).
+ *      the block loop (which would pin 160 VGPRs).  But a volatile read
+ *      cannot be sunk either: when a compression's result is only used
+ *      under a lane condition (a tail block, an HMAC key block, a store
+ *      behind `if (live)`), the compiler sinks the rounds into that branch
+ *      and leaves all 80 reads above it, live at once (HMAC-SHA512 reached
+ *      400 VGPRs);
+ *   3: as 2, but plain (non-volatile) reads through a base address offset
+ *      by an opaque per-compression zero (an `s_mov_b32 0` the compiler
+ *      cannot see through): loop-variant, so not hoisted out of the block
+ *      loop, yet free to move with the rounds that consume them.
  */
 #ifndef NET2_KM512
-#define NET2_KM512 2
+#define NET2_KM512 3
 #endif
+typedef __attribute__((address_space(3))) uint64_t lds_k64;
 __shared__ uint64_t k512_lds[160];	/* [0,80) K512, [80,160) pad K+W */
 
 /*
@@ -370,7 +380,7 @@ __shared__ uint64_t k512_lds[160];	/* [0,80) K512, [80,160) pad K+W */
  */
 __device__ __forceinline__ void k512_lds_fill()
 {
-#if NET2_KM512 == 2
+#if NET2_KM512 >= 2
 	for (unsigned i = threadIdx.x; i < 80; i += blockDim.x)
 		k512_lds[i] = K512[i];
 	__syncthreads();
@@ -380,7 +390,7 @@ __device__ __forceinline__ void k512_lds_fill()
 template <class PAD>
 __device__ __forceinline__ void k512_lds_fill_pad(const PAD &pad)
 {
-#if NET2_KM512 == 2
+#if NET2_KM512 >= 2
 	for (unsigned i = threadIdx.x; i < 80; i += blockDim.x)
 		k512_lds[i] = K512[i];
 	if (threadIdx.x < 64) {
@@ -399,31 +409,72 @@ __device__ __forceinline__ void k512_lds_fill_pad(const PAD &pad)
 #endif
 }
 
-template <int T>
-__device__ __forceinline__ uint64_t addk512(uint64_t w)
+/* Base of the LDS constant table for one compression (see NET2_KM512). */
+__device__ __forceinline__ const lds_k64 *k512_base()
 {
-#if NET2_KM512 == 2
-	typedef __attribute__((address_space(3))) volatile uint64_t lds_u64;
-	return w + ((lds_u64 *)(k512_lds))[T];
+#if NET2_KM512 == 3
+	uint32_t z;
+	asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+	return (const lds_k64 *)k512_lds + z;
 #else
-	return w + K512[T];
+	return (const lds_k64 *)k512_lds;
+#endif
+}
+
+template <int T>
+__device__ __forceinline__ uint64_t k512_at(const lds_k64 *kb)
+{
+#if NET2_KM512 == 3
+	return kb[T];
+#elif NET2_KM512 == 2
+	typedef __attribute__((address_space(3))) volatile uint64_t lds_u64;
+	return ((const lds_u64 *)kb)[T];
+#else
+	(void)kb;
+	return T < 80 ? K512[T] : 0;
+#endif
+}
+
+template <int T>
+__device__ __forceinline__ uint64_t addk512(uint64_t w, const lds_k64 *kb)
+{
+	return w + k512_at<T>(kb);
+}
+
+/*
+ * Scheduling fence every NET2_SB512 rounds.  Without it the machine
+ * scheduler may hoist all 80 LDS constant reads of a straight-line
+ * compression (a tail or HMAC block outside the block loop) to its top,
+ * which pins 160 extra VGPRs (var/HMAC SHA-512 kernels went to 220-400
+ * VGPRs, i.e. 1-2 waves per SIMD).  0 disables the fences.
+ */
+#ifndef NET2_SB512
+#define NET2_SB512 8
+#endif
+template <int T>
+__device__ __forceinline__ void fence512()
+{
+#if NET2_SB512 > 0
+	if (T % NET2_SB512 == NET2_SB512 - 1)
+		__builtin_amdgcn_sched_barrier(0);
 #endif
 }
 
 template <int T>
 struct Rounds512 {
 	__device__ __forceinline__ static void run(uint64_t (&s)[8],
-	    uint64_t (&w)[16])
+	    uint64_t (&w)[16], const lds_k64 *kb)
 	{
 		uint64_t wt = T < 16 ? w[T & 15] : expand512<T>(w);
-		round512<T>(s, addk512<T>(wt));
-		Rounds512<T + 1>::run(s, w);
+		round512<T>(s, addk512<T>(wt, kb));
+		fence512<T>();
+		Rounds512<T + 1>::run(s, w, kb);
 	}
 };
 template <>
 struct Rounds512<80> {
 	__device__ __forceinline__ static void run(uint64_t (&)[8],
-	    uint64_t (&)[16]) {}
+	    uint64_t (&)[16], const lds_k64 *) {}
 };
 
 /* SHA512Transform (src/sha2.c:663-734) on registers. */
@@ -434,7 +485,7 @@ __device__ __forceinline__ void compress512(uint64_t (&st)[8],
 #pragma unroll
 	for (int i = 0; i < 8; i++)
 		s[i] = st[i];
-	Rounds512<0>::run(s, w);
+	Rounds512<0>::run(s, w, k512_base());
 #pragma unroll
 	for (int i = 0; i < 8; i++)
 		st[i] += s[i];
@@ -443,22 +494,23 @@ __device__ __forceinline__ void compress512(uint64_t (&st)[8],
 template <int T>
 struct RoundsKW512 {
 	__device__ __forceinline__ static void run(uint64_t (&s)[8],
-	    const uint64_t *kw)
+	    const uint64_t *kw, const lds_k64 *kb)
 	{
-#if NET2_KM512 == 2
-		typedef __attribute__((address_space(3))) volatile uint64_t lds_u64;
-		round512<T>(s, ((lds_u64 *)(k512_lds))[80 + T]);
+#if NET2_KM512 >= 2
+		round512<T>(s, k512_at<80 + T>(kb));
 		(void)kw;
 #else
+		(void)kb;
 		round512<T>(s, kw[T]);
 #endif
-		RoundsKW512<T + 1>::run(s, kw);
+		fence512<T>();
+		RoundsKW512<T + 1>::run(s, kw, kb);
 	}
 };
 template <>
 struct RoundsKW512<80> {
 	__device__ __forceinline__ static void run(uint64_t (&)[8],
-	    const uint64_t *) {}
+	    const uint64_t *, const lds_k64 *) {}
 };
 
 __device__ __forceinline__ void compress512_kw(uint64_t (&st)[8],
@@ -468,7 +520,7 @@ __device__ __forceinline__ void compress512_kw(uint64_t (&st)[8],
 #pragma unroll
 	for (int i = 0; i < 8; i++)
 		s[i] = st[i];
-	RoundsKW512<0>::run(s, kw);
+	RoundsKW512<0>::run(s, kw, k512_base());
 #pragma unroll
 	for (int i = 0; i < 8; i++)
 		st[i] += s[i];

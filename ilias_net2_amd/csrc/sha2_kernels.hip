@@ -219,6 +219,19 @@ __device__ __forceinline__ void store_digest(uint8_t *o, const uint32_t (&v)[16]
 }
 
 /*
+ * Pin a finished state before a lane-conditional use (`if (live) store`):
+ * otherwise the compiler sinks the last compression into the branch and
+ * leaves its LDS constant reads (SHA-512) above it, all live at once.
+ */
+template <class H>
+__device__ __forceinline__ void materialize(const typename H::State &st)
+{
+#pragma unroll
+	for (int i = 0; i < 8; i++)
+		asm volatile("" ::"v"(st[i]));
+}
+
+/*
  * Whole-message digest for one lane.  nfull full blocks stream from p with
  * a one-block prefetch; then the generic tail (data remainder + 0x80 +
  * length, one or two blocks), or -- when the caller knows every message of
@@ -379,6 +392,7 @@ __global__ __launch_bounds__(256) void var_kernel(const uint8_t *__restrict__ ba
 		digest_one<H, AMODE_A4, false>(p, len, is384, nullptr, st);
 	else
 		digest_one<H, AMODE_A1, false>(p, len, is384, nullptr, st);
+	materialize<H>(st);
 	if (!live)
 		return;
 	uint32_t o[16];
@@ -426,27 +440,50 @@ __device__ __forceinline__ int digest_words(const typename H::State &st,
 	return is384 ? 12 : 16;
 }
 
+/* Midstate `which` (0 inner, 1 outer) from LDS into a state. */
 template <class H>
-__device__ __forceinline__ void hmac_lane(const uint8_t *p, uint32_t len,
-    int is384, bool a16, const uint32_t (*mid)[16], typename H::State &st)
+__device__ __forceinline__ void load_mid(const uint32_t (*mid)[16], int which,
+    typename H::State &st)
 {
-	constexpr int NW32 = H::NW32;
-	typename H::State outer;
+	/* opaque zero: keeps the reads where they are written (not hoisted
+	 * and shared across the address-mode branches) */
+	uint32_t z;
+	asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+	mid += z;
 #pragma unroll
 	for (int i = 0; i < 8; i++) {
-		if (sizeof(typename H::word) == 4) {
-			st[i] = mid[0][i];
-			outer[i] = mid[1][i];
-		} else {
-			st[i] = mk64(mid[0][2 * i + 1], mid[0][2 * i]);
-			outer[i] = mk64(mid[1][2 * i + 1], mid[1][2 * i]);
-		}
+		if (sizeof(typename H::word) == 4)
+			st[i] = mid[which][i];
+		else
+			st[i] = mk64(mid[which][2 * i + 1], mid[which][2 * i]);
 	}
-	if (a16)
-		absorb<H, AMODE_A16>(p, len, st);
+}
+
+/* Inner hash from the ipad midstate, one address mode. */
+template <class H, int AMODE, bool PADCONST>
+__device__ __forceinline__ void hmac_inner(const uint8_t *p, uint32_t len,
+    const uint32_t (*mid)[16], const typename H::word *kw,
+    typename H::State &st)
+{
+	load_mid<H>(mid, 0, st);
+	absorb<H, AMODE>(p, len, st);
+	finish<H, PADCONST>(p, len, ((uint64_t)len + H::BLOCK) << 3, kw, st);
+}
+
+template <class H, bool PADCONST>
+__device__ __forceinline__ void hmac_lane(const uint8_t *p, uint32_t len,
+    int is384, int amode, const uint32_t (*mid)[16],
+    const typename H::word *kw, typename H::State &st)
+{
+	constexpr int NW32 = H::NW32;
+	/* the midstates stay in LDS and are read where they are used, so
+	 * neither is held in VGPRs across the block loop */
+	if (amode == AMODE_A16)
+		hmac_inner<H, AMODE_A16, PADCONST>(p, len, mid, kw, st);
+	else if (amode == AMODE_A4)
+		hmac_inner<H, AMODE_A4, PADCONST>(p, len, mid, kw, st);
 	else
-		absorb<H, AMODE_A1>(p, len, st);
-	finish<H, false>(p, len, ((uint64_t)len + H::BLOCK) << 3, nullptr, st);
+		hmac_inner<H, AMODE_A1, PADCONST>(p, len, mid, kw, st);
 
 	/* outer: one block = inner digest || 0x80 || 0... || bit count */
 	uint32_t w[NW32];
@@ -462,41 +499,48 @@ __device__ __forceinline__ void hmac_lane(const uint8_t *p, uint32_t len,
 	const uint64_t obits = (uint64_t)(H::BLOCK + 4 * dw) << 3;
 	w[NW32 - 2] = (uint32_t)(obits >> 32);
 	w[NW32 - 1] = (uint32_t)obits;
-#pragma unroll
-	for (int i = 0; i < 8; i++)
-		st[i] = outer[i];
+	load_mid<H>(mid, 1, st);
 	H::compress(st, w);
 }
 
-template <class H>
+/*
+ * PADCONST: fixed layout with fixed_len % BLOCK == 0, so the inner pad
+ * block (bit count = (BLOCK + fixed_len) * 8) is the same for every lane
+ * and its K + W schedule comes precomputed in pad, as in fixed_kernel.
+ */
+template <class H, bool PADCONST>
 __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ base,
     const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
     const uint32_t *__restrict__ perm, uint64_t stride, uint32_t fixed_len,
     uint64_t n, uint8_t *__restrict__ out, uint32_t dlen, int is384,
-    HKey<H::NW32> key)
+    HKey<H::NW32> key, PadKW<typename H::word> pad)
 {
 	constexpr int NW32 = H::NW32;
 	__shared__ uint32_t mid[2][16];
-	if (sizeof(typename H::word) == 8)
-		k512_lds_fill();
+	if (sizeof(typename H::word) == 8) {
+		if (PADCONST)
+			k512_lds_fill_pad(pad);
+		else
+			k512_lds_fill();
+	}
 	if (threadIdx.x < 64) {
+		/* lane 0: K' ^ ipad, lane 1: K' ^ opad -- one compression */
+		const int pass = threadIdx.x & 1;
+		const uint32_t pad = pass ? 0x5c5c5c5cu : 0x36363636u;
+		typename H::State ks;
+		H::init(ks, is384);
+		uint32_t w[NW32];
 #pragma unroll
-		for (int pass = 0; pass < 2; pass++) {
-			const uint32_t pad = pass ? 0x5c5c5c5cu : 0x36363636u;
-			typename H::State ks;
-			H::init(ks, is384);
-			uint32_t w[NW32];
+		for (int i = 0; i < NW32; i++)
+			w[i] = key.w[i] ^ pad;
+		H::compress(ks, w);
+		materialize<H>(ks);
+		uint32_t kw[NW32];
+		digest_words<H>(ks, 0, kw);
+		if (threadIdx.x < 2)
 #pragma unroll
-			for (int i = 0; i < NW32; i++)
-				w[i] = key.w[i] ^ pad;
-			H::compress(ks, w);
-			uint32_t kw[NW32];
-			digest_words<H>(ks, 0, kw);
-			if (threadIdx.x == 0)
-#pragma unroll
-				for (int i = 0; i < 16; i++)
-					mid[pass][i] = i < (sizeof(typename H::word) == 4 ? 8 : 16) ? kw[i] : 0u;
-		}
+			for (int i = 0; i < 16; i++)
+				mid[pass][i] = i < (sizeof(typename H::word) == 4 ? 8 : 16) ? kw[i] : 0u;
 	}
 	__syncthreads();
 
@@ -514,8 +558,11 @@ __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ b
 		len = live ? fixed_len : 0;
 	}
 	typename H::State st;
-	hmac_lane<H>(p, len, is384,
-	    __all((reinterpret_cast<uintptr_t>(p) & 15) == 0), mid, st);
+	const uintptr_t pa = reinterpret_cast<uintptr_t>(p);
+	const int amode = __all((pa & 15) == 0) ? AMODE_A16 :
+	    __all((pa & 3) == 0) ? AMODE_A4 : AMODE_A1;
+	hmac_lane<H, PADCONST>(p, len, is384, amode, mid, pad.kw, st);
+	materialize<H>(st);
 	if (!live)
 		return;
 	uint32_t o[16];
@@ -884,20 +931,36 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 		perm = ws + 2 * NET2_SHA2_NBINS;
 	}
 	const unsigned grid = grid_for(n);
+	const bool padconst = offsets == nullptr && fixed_len % blk == 0;
+	const uint64_t ibits = ((uint64_t)fixed_len + blk) << 3;
 	if (s256) {
 		HKey<16> k;
 		for (int i = 0; i < 16; i++)
 			k.w[i] = ((uint32_t)kb[4 * i] << 24) | ((uint32_t)kb[4 * i + 1] << 16) |
 			    ((uint32_t)kb[4 * i + 2] << 8) | kb[4 * i + 3];
-		hmac_kernel<Sha256><<<grid, 256, 0, s>>>(base, offsets, lens, perm,
-		    stride, fixed_len, n, out, dlen, 0, k);
+		PadKW<uint32_t> pad = {};
+		if (padconst) {
+			pad_kw256(ibits, pad);
+			hmac_kernel<Sha256, true><<<grid, 256, 0, s>>>(base, offsets,
+			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad);
+		} else {
+			hmac_kernel<Sha256, false><<<grid, 256, 0, s>>>(base, offsets,
+			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad);
+		}
 	} else {
 		HKey<32> k;
 		for (int i = 0; i < 32; i++)
 			k.w[i] = ((uint32_t)kb[4 * i] << 24) | ((uint32_t)kb[4 * i + 1] << 16) |
 			    ((uint32_t)kb[4 * i + 2] << 8) | kb[4 * i + 3];
-		hmac_kernel<Sha512><<<grid, 256, 0, s>>>(base, offsets, lens, perm,
-		    stride, fixed_len, n, out, dlen, is384, k);
+		PadKW<uint64_t> pad = {};
+		if (padconst) {
+			pad_kw512(ibits, pad);
+			hmac_kernel<Sha512, true><<<grid, 256, 0, s>>>(base, offsets,
+			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad);
+		} else {
+			hmac_kernel<Sha512, false><<<grid, 256, 0, s>>>(base, offsets,
+			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad);
+		}
 	}
 	return hipGetLastError();
 }

@@ -295,16 +295,19 @@ def test_hmac_batches(dev, batch, oracle_mod, alg):
     import hmac as pyhmac
     hl = {4: 32, 5: 48, 6: 64}[alg]
     key = bytes(synth.random_bytes(40 + alg, hl))
-    # fixed layout across the padding boundaries
+    # fixed layout across the padding boundaries; strides that put every
+    # packet on a 16-byte (A16), 4-byte (A4) or odd (A1) address; lengths
+    # that are block multiples take the constant-pad-block kernel
     for length in (0, 1, 55, 56, 64, 111, 112, 128, 1000, 1024):
         n = 257
-        stride = length + 5
-        data = synth.fixed_batch(50 + length, n, length, stride)
-        got = batch.hmac_dev(alg, key, to_dev(data, dev), stride=stride,
-                             length=length, n=n).cpu().numpy()
-        for i in (0, 1, n // 2, n - 1):
-            msg = data[i * stride:i * stride + length].tobytes()
-            assert got[i].tobytes() == oracle_mod.hmac(alg, key, msg), (length, i)
+        for stride in (length + 5, max(16, -(-length // 16) * 16),
+                       -(-length // 4) * 4 + 4):
+            data = synth.fixed_batch(50 + length, n, length, stride)
+            got = batch.hmac_dev(alg, key, to_dev(data, dev), stride=stride,
+                                 length=length, n=n).cpu().numpy()
+            for i in range(n):
+                msg = data[i * stride:i * stride + length].tobytes()
+                assert got[i].tobytes() == oracle_mod.hmac(alg, key, msg), (length, stride, i)
         h = {4: "sha256", 5: "sha384", 6: "sha512"}[alg]
         msg = data[:length].tobytes()
         assert got[0].tobytes() == pyhmac.new(key, msg, h).digest()
