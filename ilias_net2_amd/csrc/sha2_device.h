@@ -449,7 +449,7 @@ __device__ __forceinline__ uint64_t addk512(uint64_t w, const lds_k64 *kb)
  * VGPRs, i.e. 1-2 waves per SIMD).  0 disables the fences.
  */
 #ifndef NET2_SB512
-#define NET2_SB512 8
+#define NET2_SB512 0
 #endif
 template <int T>
 __device__ __forceinline__ void fence512()
