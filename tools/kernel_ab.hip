@@ -25,6 +25,16 @@ __global__ __launch_bounds__(BS) void k_plain(const uint8_t *base, uint32_t len,
 		fixed_lane<Sha256, AMODE_A16, true>(i, base, len, len, out, 32, 0, pad.kw);
 }
 
+/* the A4 / A1 load paths on the same (16-byte aligned) packets */
+template <int AM>
+__global__ __launch_bounds__(256) void k_amode(const uint8_t *base, uint32_t len,
+    uint64_t n, uint8_t *out, KW pad)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+	if (i < n)
+		fixed_lane<Sha256, AM, true>(i, base, len, len, out, 32, 0, pad.kw);
+}
+
 template <int BS>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_num_sgpr(80)))
 void k_sgpr80(const uint8_t *base, uint32_t len, uint64_t n, uint8_t *out, KW pad)
@@ -189,6 +199,8 @@ int main()
 		{"E block64 sgpr80", [&](uint8_t *o) { k_sgpr80<64><<<n / 64, 64>>>(d_in, len, n, o, pad); }},
 		{"F stride 256x(8/CU) sgpr80", [&](uint8_t *o) { k_stride<256><<<cus * 8, 256>>>(d_in, len, n, o, pad); }},
 		{"G stride 64x(32/CU) sgpr80", [&](uint8_t *o) { k_stride<64><<<cus * 32, 64>>>(d_in, len, n, o, pad); }},
+		{"H block256 A4 (dword loads)", [&](uint8_t *o) { k_amode<AMODE_A4><<<n / 256, 256>>>(d_in, len, n, o, pad); }},
+		{"I block256 A1 (dword + alignbyte)", [&](uint8_t *o) { k_amode<AMODE_A1><<<n / 256, 256>>>(d_in, len, n, o, pad); }},
 		{"L block256 LDS-staged glds", [&](uint8_t *o) { k_lds<<<n / 256, 256>>>(d_in, len, n, o, pad); }},
 	};
 	if (do512)
