@@ -151,6 +151,16 @@ def load_pmc(config_name):
         return json.load(f)
 
 
+def load_isa_mix(config_name):
+    """Instruction mix of the config kernel's block loop, priced with the
+    probed issue costs (profiles/isa_mix.json, written by tools/isa_mix.py)."""
+    path = os.path.join(ROOT, "profiles", "isa_mix.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)["configs"].get(config_name)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -285,6 +295,18 @@ def main():
                 "clock_ghz": round(clk, 3),
                 "instr_per_launch": instr,
                 "source": "rocprofv3 SQ_INSTS_VALU / GRBM_GUI_ACTIVE, profiles/pmc_%s.json" % args.config}
+        mix = load_isa_mix(args.config)
+        if mix and mix.get("mean_issue_cycles_per_valu_instr"):
+            # Issue floor: every VALU instruction of the launch priced at the
+            # mean measured cost of the block loop's mix (tools/isa_mix.py,
+            # probe costs normalised to 2.4 GHz like the probe itself).
+            m = mix["mean_issue_cycles_per_valu_instr"]
+            floor_ms = instr / 1024 * m / 2.4e9 * 1e3
+            valu["issue_floor"] = {
+                "mean_cycles_per_valu_instr": m,
+                "floor_ms": round(floor_ms, 4),
+                "frac": round(floor_ms / launch_ms, 4),
+                "source": "profiles/isa_mix.json (loop mix) x profiles/round1/valu_probe.json (costs)"}
 
     line = {
         "metric": METRIC if args.config == "c2" else

@@ -303,11 +303,18 @@ __device__ __forceinline__ uint64_t bsig1_512(uint64_t e)
 /*
  * 64-bit logical shift as one v_lshrrev_b64 (hipcc otherwise emits
  * v_alignbit_b32 + v_lshrrev_b32, two VALU ops for the same result).
+ * Issue costs (tools/valu_probe): v_lshrrev_b64 4.2 SIMD cycles per wave
+ * instruction against 4.3 + 2.6 for the pair; measured -2% on the SHA-512
+ * fixed kernel (profiles/round1/sha512_u2_shr_ab.json).  NET2_SHR64_ASM=0
+ * restores the plain C shift.
  */
+#ifndef NET2_SHR64_ASM
+#define NET2_SHR64_ASM 1
+#endif
 template <int N>
 __device__ __forceinline__ uint64_t shr64(uint64_t x)
 {
-#ifdef NET2_SHR64_ASM
+#if NET2_SHR64_ASM
 	uint64_t r;
 	asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(N), "v"(x));
 	return r;

@@ -243,6 +243,11 @@ __device__ __forceinline__ void materialize(const typename H::State &st)
  * whole blocks are transformed straight from caller memory).  With
  * PREFETCH, block k+1 is loaded while block k is compressed.
  */
+/* 1: two blocks per loop trip (no prefetch-buffer copies): -1.5% on C2,
+ * profiles/round1/sha256_u2_ab.json.  0: the one-block loop. */
+#ifndef NET2_ABSORB_U2
+#define NET2_ABSORB_U2 1
+#endif
 template <class H, int AMODE, bool PREFETCH = H::PREFETCH>
 __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
     typename H::State &st)
@@ -250,7 +255,40 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 	constexpr int NW32 = H::NW32;
 	const uint32_t nfull = len / H::BLOCK;
 
-	if (PREFETCH) {
+	if (PREFETCH && NET2_ABSORB_U2) {
+		/*
+		 * Two blocks per trip with the buffers swapping roles, so the
+		 * prefetched block is consumed where it landed (a one-block loop
+		 * copies it over: 16 v_mov per block).
+		 */
+		Raw<NW32> ra, rb;
+		if (nfull > 0)
+			issue_block<NW32, AMODE>(p, ra);
+		uint32_t k = 0;
+		for (; k + 2 <= nfull; k += 2) {
+			const uint8_t *bp = p + (size_t)k * H::BLOCK;
+			issue_block<NW32, AMODE>(bp + H::BLOCK, rb);
+			uint32_t w[NW32];
+			finish_block<NW32, AMODE>(bp, ra, w);
+			H::compress(st, w);
+			/*
+			 * Unconditional, so ra is always (re)defined here: a
+			 * conditional load makes ra a phi and brings the copies
+			 * back.  Past the last block it re-reads block k + 1
+			 * (in bounds, L2-hot) and the result is unused.
+			 */
+			issue_block<NW32, AMODE>(bp + (k + 2 < nfull ? 2 : 1) *
+			    H::BLOCK, ra);
+			uint32_t w2[NW32];
+			finish_block<NW32, AMODE>(bp + H::BLOCK, rb, w2);
+			H::compress(st, w2);
+		}
+		if (k < nfull) {
+			uint32_t w[NW32];
+			finish_block<NW32, AMODE>(p + (size_t)k * H::BLOCK, ra, w);
+			H::compress(st, w);
+		}
+	} else if (PREFETCH) {
 		Raw<NW32> cur;
 		if (nfull > 0)
 			issue_block<NW32, AMODE>(p, cur);
@@ -886,8 +924,6 @@ hipError_t net2_launch_var(int alg, const uint8_t *base,
 	if (n == 0)
 		return hipSuccess;
 	const bool s256 = alg == NET2_ALG_SHA256;
-	const int blk_shift = s256 ? 6 : 7;
-	const int lenbytes = s256 ? 8 : 16;
 	const int is384 = alg == NET2_ALG_SHA384;
 	const uint32_t dlen = s256 ? 32 : is384 ? 48 : 64;
 	uint32_t *perm = nullptr;

@@ -1,0 +1,196 @@
+#!/usr/bin/env python3
+"""VALU issue floor of the shipped kernels, from their gfx950 ISA.
+
+The SHA kernels are bound by vector-instruction issue, not by HBM (DESIGN.md
+5.3).  Their floor is therefore a sum over the instructions a wave issues of
+what each one costs the SIMD.  This tool:
+
+  1. reads the device assembly of sha2_kernels.hip (`make -C
+     ilias_net2_amd/csrc asm` writes ilias_net2_amd/csrc/build/sha2_kernels.s),
+  2. for each bench config's kernel, counts the VALU instructions of its
+     innermost loop body (the block loop: >94 % of the instructions a C2/C4
+     wave issues) by mnemonic and operand form,
+  3. prices them with the issue costs measured by tools/valu_probe.hip
+     (profiles/round1/valu_probe.json: SIMD cycles per wave64 instruction,
+     8 waves/SIMD, independent chains),
+  4. writes profiles/isa_mix.json: per config, the loop's instruction mix and
+     its mean issue cost per VALU instruction (cycles).
+
+bench.py multiplies that mean by the launch's SQ_INSTS_VALU (rocprofv3) to
+get the launch's issue floor, and reports the measured launch against it.
+The model is additive (costs of a mixed stream add up); the probe's "mix"
+rows show it holds to within about +-10 % per pair, in both directions.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+from collections import Counter
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ASM = os.path.join(ROOT, "ilias_net2_amd", "csrc", "build", "sha2_kernels.s")
+PROBE = os.path.join(ROOT, "profiles", "round1", "valu_probe.json")
+OUT = os.path.join(ROOT, "profiles", "isa_mix.json")
+
+# bench config -> mangled-name prefix of the kernel instance it launches
+KERNELS = {
+    "c2": "_ZN4net23dev12fixed_kernelINS0_6Sha256ELi0ELb1E",
+    "c4": "_ZN4net23dev12fixed_kernelINS0_6Sha512ELi0ELb1E",
+    "c3": "_ZN4net23dev10var_kernelINS0_6Sha256E",
+    "hmac": "_ZN4net23dev11hmac_kernelINS0_6Sha256ELb1E",
+    "hmac_mtu": "_ZN4net23dev11hmac_kernelINS0_6Sha256ELb0E",
+    "hmac512": "_ZN4net23dev11hmac_kernelINS0_6Sha512ELb1E",
+    "hmac512_mtu": "_ZN4net23dev11hmac_kernelINS0_6Sha512ELb0E",
+}
+
+# probe row name -> (mnemonic, operand form); form "v" = VGPR/inline-constant
+# sources only, "s" = an SGPR source, "lit" = a 32-bit literal.
+PROBE_ROWS = {
+    "v_add_u32 (VOP2, v,v)": ("v_add_u32", "v"),
+    "v_add_u32 literal": ("v_add_u32", "lit"),
+    "v_add_u32 s": ("v_add_u32", "s"),
+    "v_xor_b32 (VOP2)": ("v_xor_b32", "v"),
+    "v_or_b32 (VOP2)": ("v_or_b32", "v"),
+    "v_and_b32": ("v_and_b32", "v"),
+    "v_not_b32": ("v_not_b32", "v"),
+    "v_sub_u32": ("v_sub_u32", "v"),
+    "v_mov_b32": ("v_mov_b32", "v"),
+    "v_lshrrev_b32 (VOP2, imm)": ("v_lshrrev_b32", "v"),
+    "v_lshlrev_b32 (VOP2, imm)": ("v_lshlrev_b32", "v"),
+    "v_bitop3_b32 xor3 (3 v)": ("v_bitop3_b32", "v"),
+    "v_alignbit_b32 x,x,imm (rotate)": ("v_alignbit_b32", "v"),
+    "v_alignbit_b32 x,x,s": ("v_alignbit_b32", "s"),
+    "v_alignbyte_b32 imm": ("v_alignbyte_b32", "v"),
+    "v_add3_u32 v,v,v": ("v_add3_u32", "v"),
+    "v_add3_u32 v,v,s": ("v_add3_u32", "s"),
+    "v_perm_b32 0,v,s (bswap)": ("v_perm_b32", "s"),
+    "v_bfi_b32": ("v_bfi_b32", "v"),
+    "v_lshl_or_b32 v,imm,v": ("v_lshl_or_b32", "v"),
+    "v_and_or_b32": ("v_and_or_b32", "v"),
+    "v_or3_b32": ("v_or3_b32", "v"),
+    "v_xad_u32": ("v_xad_u32", "v"),
+    "v_lshl_add_u64 v,0,v (64-bit add)": ("v_lshl_add_u64", "v"),
+    "v_lshl_add_u64 v,0,s": ("v_lshl_add_u64", "s"),
+    "v_lshrrev_b64 imm": ("v_lshrrev_b64", "v"),
+    "v_add_f32": ("v_add_f32", "v"),
+}
+# Instructions whose VGPR/SGPR forms measured the same (cost of either row).
+SAME_FORMS = {"v_alignbit_b32", "v_add3_u32", "v_perm_b32", "v_lshl_add_u64"}
+
+
+def cost_table(probe_path=PROBE):
+    with open(probe_path) as f:
+        rows = json.load(f)["results"]
+    t = {}
+    for r in rows:
+        if r["waves_per_simd"] != 8 or r["op"] not in PROBE_ROWS:
+            continue
+        t[PROBE_ROWS[r["op"]]] = r["simd_cycles_per_wave_instr_at_2.4GHz"]
+    # bitop3: mean of the two truth tables measured (xor3 0x96, ch 0xca)
+    b3 = [r["simd_cycles_per_wave_instr_at_2.4GHz"] for r in rows
+          if r["waves_per_simd"] == 8 and r["op"].startswith("v_bitop3_b32")]
+    t[("v_bitop3_b32", "v")] = sum(b3) / len(b3)
+    return t
+
+
+def kernel_body(lines, prefix):
+    start = next(i for i, ln in enumerate(lines)
+                 if ln.startswith(prefix) and re.match(r"^\S+:(\s|$)", ln))
+    end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
+    return lines[start:end + 1]
+
+
+def innermost_loop(body):
+    """Lines of the innermost (deepest) loop: from its header label to the
+    branch back to it."""
+    best = None
+    for i, ln in enumerate(body):
+        m = re.match(r"^(\.LBB\d+_\d+):.*Loop Header: Depth=(\d+)", ln)
+        if not m:
+            continue
+        label, depth = m.group(1), int(m.group(2))
+        back = max(j for j, l2 in enumerate(body) if re.search(
+            r"s_c?branch\w*\s+" + re.escape(label) + r"$", l2.strip()))
+        n_valu = sum(1 for l2 in body[i:back + 1] if l2.strip().startswith("v_"))
+        key = (depth, n_valu)
+        if best is None or key > best[0]:
+            best = (key, body[i:back + 1])
+    return best[1] if best else []
+
+
+def classify(line):
+    parts = line.strip().split(None, 1)
+    mn = re.sub(r"_e(32|64)$", "", parts[0])
+    ops = parts[1].split(",")[1:] if len(parts) > 1 else []
+    form = "v"
+    for o in ops:
+        o = o.strip().split()[0] if o.strip() else ""
+        if re.match(r"^s(\d+|\[)", o):
+            form = "s"
+        elif re.match(r"^0x[0-9a-f]+$", o) and int(o, 16) > 64:
+            form = "lit" if form == "v" else form
+    return mn, form
+
+
+def price(mn, form, table):
+    if (mn, form) in table:
+        return table[(mn, form)], "measured"
+    if mn in SAME_FORMS:
+        for f in ("v", "s"):
+            if (mn, f) in table:
+                return table[(mn, f)], "measured (other operand form)"
+    if (mn, "v") in table and form == "lit":
+        return table[(mn, "v")], "measured (VGPR form)"
+    if (mn, "v") in table and form == "s":
+        # an SGPR source moved every fast VOP2 probe to the slow class
+        return max(table[(mn, "v")], table[("v_add_u32", "s")]), "VOP2+SGPR class"
+    return 4.3, "unprobed: slow-class cost assumed"
+
+
+def analyse(lines, prefix, table):
+    body = kernel_body(lines, prefix)
+    loop = innermost_loop(body)
+    mix = Counter()
+    for ln in loop:
+        s = ln.strip()
+        if s.startswith("v_"):
+            mix[classify(s)] += 1
+    total_instr = sum(mix.values())
+    cyc = 0.0
+    rows = []
+    for (mn, form), n in sorted(mix.items(), key=lambda kv: -kv[1]):
+        c, how = price(mn, form, table)
+        cyc += c * n
+        rows.append({"instr": mn, "operands": form, "count": n,
+                     "cycles_each": round(c, 3), "priced": how})
+    return {"kernel": prefix, "loop_valu_instr": total_instr,
+            "loop_issue_cycles": round(cyc, 1),
+            "mean_issue_cycles_per_valu_instr": round(cyc / total_instr, 4) if total_instr else None,
+            "mix": rows}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--asm", default=ASM)
+    ap.add_argument("--out", default=OUT)
+    args = ap.parse_args()
+    with open(args.asm) as f:
+        lines = f.read().splitlines()
+    table = cost_table()
+    res = {"source": "tools/isa_mix.py over `make asm` output; costs from "
+                     "profiles/round1/valu_probe.json (SIMD cycles per wave64 "
+                     "instruction at 2.4 GHz, 8 waves/SIMD)",
+           "configs": {}}
+    for cfg, prefix in KERNELS.items():
+        res["configs"][cfg] = analyse(lines, prefix, table)
+        r = res["configs"][cfg]
+        print(f"{cfg:12s} loop VALU {r['loop_valu_instr']:5d}  mean "
+              f"{r['mean_issue_cycles_per_valu_instr']} cyc/instr")
+    with open(args.out, "w") as f:
+        json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -48,7 +48,24 @@
 	if (K == 28) { if (c & 1) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(r[c]) : "v"(b), "v"(d)); \
 	               else asm volatile("v_add_u32 %0, %0, %1" : "+v"(r[c]) : "v"(b)); } \
 	if (K == 29) { if (c & 1) asm volatile("v_alignbit_b32 %0, %0, %0, 7" : "+v"(r[c])); \
-	               else asm volatile("v_lshrrev_b32 %0, 7, %0" : "+v"(r[c])); }
+	               else asm volatile("v_lshrrev_b32 %0, 7, %0" : "+v"(r[c])); } \
+	if (K == 30) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(q[c]) : "v"(bq)); \
+	if (K == 31) asm volatile("v_add_co_u32_e32 %0, vcc, %0, %2\n\tv_addc_co_u32_e32 %1, vcc, %1, %3, vcc" \
+	                          : "+v"(r[c]), "+v"(r2[c]) : "v"(b), "v"(d) : "vcc"); \
+	if (K == 32) asm volatile("v_lshrrev_b64 %0, 7, %0" : "+v"(q[c])); \
+	if (K == 33) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(q[c]) : "s"(sq)); \
+	if (K == 34) asm volatile("v_alignbit_b32 %0, %0, %0, %1" : "+v"(r[c]) : "s"(s)); \
+	if (K == 35) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(q[c]) : "v"(bq)); \
+	if (K == 36) asm volatile("v_add_f32_e32 %0, %0, %1" : "+v"(r[c]) : "v"(b)); \
+	if (K == 37) asm volatile("v_and_b32_e32 %0, %0, %1" : "+v"(r[c]) : "v"(b)); \
+	if (K == 38) asm volatile("v_not_b32_e32 %0, %0" : "+v"(r[c])); \
+	if (K == 39) asm volatile("v_sub_u32_e32 %0, %0, %1" : "+v"(r[c]) : "v"(b)); \
+	if (K == 40) { if (c & 1) asm volatile("v_alignbit_b32 %0, %0, %0, 7" : "+v"(r[c])); \
+	               else asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(r[c]) : "v"(b), "v"(d)); } \
+	if (K == 41) { if (c & 1) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(r[c]) : "v"(b), "v"(d)); \
+	               else asm volatile("v_add_u32 %0, %0, %1" : "+v"(r[c]) : "v"(b)); } \
+	if (K == 42) asm volatile("v_lshlrev_b32_e32 %0, %1, %0" : "+v"(r[c]) : "v"(b)); \
+	if (K == 43) asm volatile("v_mul_u32_u24_e32 %0, 0x80, %0" : "+v"(r[c]));
 
 static const char *kNames[] = {
 	"v_add_u32 (VOP2, v,v)", "v_xor_b32 (VOP2)", "v_lshrrev_b32 (VOP2, imm)",
@@ -62,19 +79,27 @@ static const char *kNames[] = {
 	"v_lshrrev_b32_e64",
 	"mix alignbit|xor 1:1", "mix alignbit|add3 1:1", "mix alignbit|xor 1:2",
 	"mix bitop3|add 1:1", "mix alignbit|lshr 1:1",
+	"v_lshl_add_u64 v,0,v (64-bit add)", "v_add_co_u32 + v_addc_co_u32 (VOP2 pair, per instr)",
+	"v_lshrrev_b64 imm", "v_lshl_add_u64 v,0,s", "v_alignbit_b32 x,x,s",
+	"v_pk_add_f32", "v_add_f32", "v_and_b32", "v_not_b32", "v_sub_u32",
+	"mix alignbit|bitop3 1:1", "mix add3|add 1:1", "v_lshlrev_b32 v,v (VOP2 var shift)",
+	"v_mul_u32_u24 literal",
 };
-#define NK 30
+#define NK 44
 
 template <int K>
 __global__ __launch_bounds__(256) void probe(uint32_t *out, uint32_t seed)
 {
 	uint64_t t0 = __builtin_amdgcn_s_memtime();
-	uint32_t r[CHAINS];
+	uint32_t r[CHAINS], r2[CHAINS];
+	uint64_t q[CHAINS];
+	uint64_t bq = ((uint64_t)seed << 32) ^ threadIdx.x;
+	uint64_t sq = __builtin_amdgcn_readfirstlane(seed * 5 + 1);
 	uint32_t b = seed ^ threadIdx.x, d = seed * 7 + threadIdx.x;
 	uint32_t s = __builtin_amdgcn_readfirstlane(seed * 3 + 1);
 #pragma unroll
 	for (int c = 0; c < CHAINS; c++)
-		r[c] = threadIdx.x * (c + 1);
+		r[c] = threadIdx.x * (c + 1), r2[c] = r[c] ^ seed, q[c] = ((uint64_t)r[c] << 32) | r2[c];
 	for (int it = 0; it < ITERS; it++) {
 #pragma unroll
 		for (int c = 0; c < CHAINS; c++) {
@@ -84,7 +109,7 @@ __global__ __launch_bounds__(256) void probe(uint32_t *out, uint32_t seed)
 	uint32_t x = 0;
 #pragma unroll
 	for (int c = 0; c < CHAINS; c++)
-		x ^= r[c];
+		x ^= r[c] ^ r2[c] ^ (uint32_t)q[c] ^ (uint32_t)(q[c] >> 32);
 	if (x == 0x12345678u)
 		out[0] = x;
 	uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -115,7 +140,7 @@ static void run(uint32_t *out, int cus, int wps, bool last)
 {
 	const int blocks = cus * wps;  // wps blocks of 4 waves per CU -> wps waves / SIMD
 	float ms = time_kernel([&] { probe<K><<<blocks, 256>>>(out, 1); });
-	double instr = (double)blocks * 4 * ITERS * CHAINS;       // wave instructions
+	double instr = (double)blocks * 4 * ITERS * CHAINS * (K == 31 ? 2 : 1);  // wave instructions
 	// cycles per wave-instruction per SIMD at the nominal 2.4 GHz
 	double cyc = ms * 1e-3 * 2.4e9 * cus * 4 / instr;
 	// clock-independent: median per-wave s_memtime span / (wps * instr per wave)
@@ -124,7 +149,7 @@ static void run(uint32_t *out, int cus, int wps, bool last)
 	std::vector<uint32_t> v(h + 16, h + 16 + blocks * 4);
 	std::sort(v.begin(), v.end());
 	double span = v[v.size() / 2];
-	double memcyc = span / (wps * (double)ITERS * CHAINS);
+	double memcyc = span / (wps * (double)ITERS * CHAINS * (K == 31 ? 2 : 1));
 	double clk = (double)v[v.size() - 1] / (ms * 1e-3) / 1e9;
 	printf("  {\"op\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.4f, "
 	    "\"simd_cycles_per_wave_instr_at_2.4GHz\": %.3f, \"memtime_cycles_per_wave_instr\": %.3f, \"memtime_GHz_est\": %.3f}%s\n",
