@@ -12,6 +12,9 @@ import os
 
 LIB_NAME = "libnet2_sha2.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# Build-variant A/B runs (tools/gpu_ab_lib.sh) point this at another build of
+# the same library; unset, the in-tree library is the one loaded.
+LIB_PATH = os.environ.get("NET2_SHA2_LIB", LIB_PATH)
 
 # Registry rows (include/net2/sha2_batch.h, include/net2/hash.h).
 NIL, SHA256, SHA384, SHA512 = 0, 1, 2, 3

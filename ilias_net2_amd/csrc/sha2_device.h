@@ -147,44 +147,121 @@ __device__ __forceinline__ uint32_t ssig1_256(uint32_t x)
  * already summed where the caller can (constant pad block), else the
  * caller passes K and W separately.
  */
-template <int T>
+/*
+ * NET2_ASM256 = 1: the body of a round (and of a schedule word) is one
+ * inline-asm block with a fixed instruction order: the six rotates of e and
+ * a are independent of each other and are issued back to back, Ch/Maj and
+ * the Sigma xors fill in between, the adds come last.  Left to itself the
+ * machine scheduler orders each Sigma as rotate, rotate, rotate, xor --
+ * every xor right behind the rotates it consumes -- and the same
+ * instructions run 5 % slower (tools/sha_variants.hip V0 vs V6/V7,
+ * profiles/round1/sha256_round_variants.json: identical instruction
+ * multiset, only the order differs).  h + K + W stays outside the block so
+ * the compiler can take K (or the pad block's K + W) from an SGPR.
+ */
+#ifndef NET2_ASM256
+#define NET2_ASM256 1
+#endif
+#ifndef NET2_FENCE256
+#define NET2_FENCE256 2
+#endif
+
+/* The round body as one asm block (see NET2_ASM256). */
+__device__ __forceinline__ void round256_asm(uint32_t a, uint32_t b,
+    uint32_t c, uint32_t &d, uint32_t e, uint32_t f, uint32_t g,
+    uint32_t &h, uint32_t x)
+{
+	uint32_t r1, r2, r3, r4, r5;
+	asm("v_alignbit_b32 %[r1], %[e], %[e], 6\n\t"
+	    "v_alignbit_b32 %[r2], %[e], %[e], 11\n\t"
+	    "v_alignbit_b32 %[r3], %[e], %[e], 25\n\t"
+	    "v_alignbit_b32 %[r4], %[a], %[a], 2\n\t"
+	    "v_alignbit_b32 %[r5], %[a], %[a], 13\n\t"
+	    "v_bitop3_b32 %[r1], %[r1], %[r2], %[r3] bitop3:0x96\n\t"
+	    "v_alignbit_b32 %[r2], %[a], %[a], 22\n\t"
+	    "v_bitop3_b32 %[r3], %[e], %[f], %[g] bitop3:0xca\n\t"
+	    "v_bitop3_b32 %[r4], %[r4], %[r5], %[r2] bitop3:0x96\n\t"
+	    "v_bitop3_b32 %[r5], %[a], %[b], %[c] bitop3:0xe8\n\t"
+	    "v_add3_u32 %[r1], %[x], %[r1], %[r3]\n\t"
+	    "v_add_u32 %[d], %[d], %[r1]\n\t"
+	    "v_add3_u32 %[h], %[r1], %[r4], %[r5]"
+	    : [r1] "=&v"(r1), [r2] "=&v"(r2), [r3] "=&v"(r3), [r4] "=&v"(r4),
+	      [r5] "=&v"(r5), [h] "=v"(h), [d] "+v"(d)
+	    : [a] "v"(a), [b] "v"(b), [c] "v"(c), [e] "v"(e), [f] "v"(f),
+	      [g] "v"(g), [x] "v"(x));
+}
+
+template <int T, bool ASM = NET2_ASM256>
 __device__ __forceinline__ void round256(uint32_t (&s)[8], uint32_t k,
     uint32_t w)
 {
 	uint32_t &a = s[(0 - T) & 7], &b = s[(1 - T) & 7], &c = s[(2 - T) & 7];
 	uint32_t &d = s[(3 - T) & 7], &e = s[(4 - T) & 7], &f = s[(5 - T) & 7];
 	uint32_t &g = s[(6 - T) & 7], &h = s[(7 - T) & 7];
-	uint32_t t1 = add3(add3(h, k, w), bsig1_256(e), ch32(e, f, g));
-	d += t1;
-	h = add3(t1, bsig0_256(a), maj32(a, b, c));
+	if (ASM) {
+		round256_asm(a, b, c, d, e, f, g, h, add3(h, k, w));
+	} else {
+		uint32_t t1 = add3(add3(h, k, w), bsig1_256(e), ch32(e, f, g));
+		d += t1;
+		h = add3(t1, bsig0_256(a), maj32(a, b, c));
+	}
+}
+
+/* sigma1(y) + w7 + sigma0(x) + w16 as one asm block (see NET2_ASM256). */
+__device__ __forceinline__ void expand256_asm(uint32_t &w16, uint32_t w7,
+    uint32_t x, uint32_t y)
+{
+	uint32_t r1, r2, r3, r4, r5, r6;
+	asm("v_alignbit_b32 %[r1], %[y], %[y], 17\n\t"
+	    "v_alignbit_b32 %[r2], %[y], %[y], 19\n\t"
+	    "v_alignbit_b32 %[r3], %[x], %[x], 7\n\t"
+	    "v_alignbit_b32 %[r4], %[x], %[x], 18\n\t"
+	    "v_lshrrev_b32 %[r5], 10, %[y]\n\t"
+	    "v_lshrrev_b32 %[r6], 3, %[x]\n\t"
+	    "v_bitop3_b32 %[r1], %[r1], %[r2], %[r5] bitop3:0x96\n\t"
+	    "v_bitop3_b32 %[r3], %[r3], %[r4], %[r6] bitop3:0x96\n\t"
+	    "v_add3_u32 %[w16], %[w16], %[r1], %[w7]\n\t"
+	    "v_add_u32 %[w16], %[w16], %[r3]"
+	    : [r1] "=&v"(r1), [r2] "=&v"(r2), [r3] "=&v"(r3), [r4] "=&v"(r4),
+	      [r5] "=&v"(r5), [r6] "=&v"(r6), [w16] "+v"(w16)
+	    : [x] "v"(x), [y] "v"(y), [w7] "v"(w7));
 }
 
 /* W[t & 15] for t >= 16, in place over the 16-word circular schedule. */
-template <int T>
+template <int T, bool ASM = NET2_ASM256>
 __device__ __forceinline__ uint32_t expand256(uint32_t (&w)[16])
 {
-	w[T & 15] = add3(w[T & 15], ssig1_256(w[(T - 2) & 15]),
-	    w[(T - 7) & 15] + ssig0_256(w[(T - 15) & 15]));
+	if (ASM)
+		expand256_asm(w[T & 15], w[(T - 7) & 15], w[(T - 15) & 15],
+		    w[(T - 2) & 15]);
+	else
+		w[T & 15] = add3(w[T & 15], ssig1_256(w[(T - 2) & 15]),
+		    w[(T - 7) & 15] + ssig0_256(w[(T - 15) & 15]));
 	return w[T & 15];
 }
 
-template <int T>
+template <int T, bool ASM>
 struct Rounds256 {
 	__device__ __forceinline__ static void run(uint32_t (&s)[8],
 	    uint32_t (&w)[16])
 	{
-		uint32_t wt = T < 16 ? w[T & 15] : expand256<T>(w);
-		round256<T>(s, K256[T], wt);
-		Rounds256<T + 1>::run(s, w);
+		uint32_t wt = T < 16 ? w[T & 15] : expand256<T, ASM>(w);
+		round256<T, ASM>(s, K256[T], wt);
+		/* keep the schedule words from being computed far ahead of
+		 * their rounds (register pressure: 8 waves/SIMD need <= 64) */
+		if (ASM && NET2_FENCE256 > 0 && T % NET2_FENCE256 == NET2_FENCE256 - 1)
+			__builtin_amdgcn_sched_barrier(0);
+		Rounds256<T + 1, ASM>::run(s, w);
 	}
 };
-template <>
-struct Rounds256<64> {
+template <bool ASM>
+struct Rounds256<64, ASM> {
 	__device__ __forceinline__ static void run(uint32_t (&)[8],
 	    uint32_t (&)[16]) {}
 };
 
 /* SHA256Transform (src/sha2.c:374-445) on registers: st += F(st, w). */
+template <bool ASM = NET2_ASM256>
 __device__ __forceinline__ void compress256(uint32_t (&st)[8],
     uint32_t (&w)[16])
 {
@@ -192,7 +269,7 @@ __device__ __forceinline__ void compress256(uint32_t (&st)[8],
 #pragma unroll
 	for (int i = 0; i < 8; i++)
 		s[i] = st[i];
-	Rounds256<0>::run(s, w);
+	Rounds256<0, ASM>::run(s, w);
 	/* After 64 rounds the renaming has wrapped around (64 % 8 == 0). */
 #pragma unroll
 	for (int i = 0; i < 8; i++)
@@ -204,21 +281,24 @@ __device__ __forceinline__ void compress256(uint32_t (&st)[8],
  * constant padding block of a length that is a multiple of 64): kw[t] =
  * K[t] + W[t] comes precomputed from the host, so no expansion runs.
  */
-template <int T>
+template <int T, bool ASM>
 struct RoundsKW256 {
 	__device__ __forceinline__ static void run(uint32_t (&s)[8],
 	    const uint32_t *kw)
 	{
-		round256<T>(s, kw[T], 0u);
-		RoundsKW256<T + 1>::run(s, kw);
+		round256<T, ASM>(s, kw[T], 0u);
+		if (ASM && NET2_FENCE256 > 0 && T % NET2_FENCE256 == NET2_FENCE256 - 1)
+			__builtin_amdgcn_sched_barrier(0);
+		RoundsKW256<T + 1, ASM>::run(s, kw);
 	}
 };
-template <>
-struct RoundsKW256<64> {
+template <bool ASM>
+struct RoundsKW256<64, ASM> {
 	__device__ __forceinline__ static void run(uint32_t (&)[8],
 	    const uint32_t *) {}
 };
 
+template <bool ASM = NET2_ASM256>
 __device__ __forceinline__ void compress256_kw(uint32_t (&st)[8],
     const uint32_t *kw)
 {
@@ -226,7 +306,7 @@ __device__ __forceinline__ void compress256_kw(uint32_t (&st)[8],
 #pragma unroll
 	for (int i = 0; i < 8; i++)
 		s[i] = st[i];
-	RoundsKW256<0>::run(s, kw);
+	RoundsKW256<0, ASM>::run(s, kw);
 #pragma unroll
 	for (int i = 0; i < 8; i++)
 		st[i] += s[i];

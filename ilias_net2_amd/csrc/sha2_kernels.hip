@@ -32,7 +32,15 @@ namespace dev {
 
 /* ---- hash traits ------------------------------------------------------ */
 
-struct Sha256 {
+/*
+ * Per-kernel code-shape choices (each measured):
+ *   ASM: round bodies as ordered asm blocks (NET2_ASM256, sha2_device.h);
+ *   U2:  the two-block ping-pong block loop (absorb below).
+ */
+template <bool ASM_, bool U2_>
+struct Sha256T {
+	static constexpr bool ASM = ASM_;
+	static constexpr bool U2 = U2_;
 	typedef uint32_t word;
 	static constexpr int BLOCK = 64;	/* bytes per block */
 	static constexpr int NW32 = 16;		/* 32-bit words per block */
@@ -51,7 +59,7 @@ struct Sha256 {
 	__device__ __forceinline__ static void compress(State &st,
 	    uint32_t (&b)[16])
 	{
-		compress256(st, b);
+		compress256<ASM>(st, b);
 	}
 	/* Store state big-endian (src/sha2.c:553-557) as 32-bit words. */
 	__device__ __forceinline__ static void out_words(const State &st,
@@ -62,8 +70,28 @@ struct Sha256 {
 			o[i] = bswap32(st[i]);
 	}
 };
+#ifndef NET2_ABSORB_U2
+#define NET2_ABSORB_U2 1
+#endif
+#ifndef NET2_VAR_ASM
+#define NET2_VAR_ASM 0
+#endif
+#ifndef NET2_VAR_U2
+#define NET2_VAR_U2 0
+#endif
+#ifndef NET2_HMAC_ASM
+#define NET2_HMAC_ASM 1
+#endif
+#ifndef NET2_HMAC_U2
+#define NET2_HMAC_U2 1
+#endif
+typedef Sha256T<NET2_ASM256 != 0, NET2_ABSORB_U2 != 0> Sha256;	/* fixed */
+typedef Sha256T<NET2_VAR_ASM != 0, NET2_VAR_U2 != 0> Sha256V;	/* var */
+typedef Sha256T<NET2_HMAC_ASM != 0, NET2_HMAC_U2 != 0> Sha256H;	/* HMAC */
 
 struct Sha512 {
+	static constexpr bool ASM = false;
+	static constexpr bool U2 = false;	/* no prefetch: nothing to ping-pong */
 	typedef uint64_t word;
 	static constexpr int BLOCK = 128;
 	static constexpr int NW32 = 32;
@@ -243,11 +271,6 @@ __device__ __forceinline__ void materialize(const typename H::State &st)
  * whole blocks are transformed straight from caller memory).  With
  * PREFETCH, block k+1 is loaded while block k is compressed.
  */
-/* 1: two blocks per loop trip (no prefetch-buffer copies): -1.5% on C2,
- * profiles/round1/sha256_u2_ab.json.  0: the one-block loop. */
-#ifndef NET2_ABSORB_U2
-#define NET2_ABSORB_U2 1
-#endif
 template <class H, int AMODE, bool PREFETCH = H::PREFETCH>
 __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
     typename H::State &st)
@@ -255,7 +278,7 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 	constexpr int NW32 = H::NW32;
 	const uint32_t nfull = len / H::BLOCK;
 
-	if (PREFETCH && NET2_ABSORB_U2) {
+	if (PREFETCH && H::U2) {
 		/*
 		 * Two blocks per trip with the buffers swapping roles, so the
 		 * prefetched block is consumed where it landed (a one-block loop
@@ -328,7 +351,7 @@ __device__ __forceinline__ void finish(const uint8_t *p, uint32_t len,
 	constexpr int NW32 = H::NW32;
 	if (PADCONST) {
 		if (sizeof(typename H::word) == 4)
-			compress256_kw(*reinterpret_cast<uint32_t(*)[8]>(&st),
+			compress256_kw<H::ASM>(*reinterpret_cast<uint32_t(*)[8]>(&st),
 			    reinterpret_cast<const uint32_t *>(kw));
 		else
 			compress512_kw(*reinterpret_cast<uint64_t(*)[8]>(&st),
@@ -935,7 +958,7 @@ hipError_t net2_launch_var(int alg, const uint8_t *base,
 		perm = ws + 2 * NET2_SHA2_NBINS;
 	}
 	if (s256)
-		var_kernel<Sha256><<<grid_for(n), 256, 0, s>>>(base, offsets,
+		var_kernel<Sha256V><<<grid_for(n), 256, 0, s>>>(base, offsets,
 		    lens, perm, n, out, dlen, 0);
 	else
 		var_kernel<Sha512><<<grid_for(n), 256, 0, s>>>(base, offsets,
@@ -977,10 +1000,10 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 		PadKW<uint32_t> pad = {};
 		if (padconst) {
 			pad_kw256(ibits, pad);
-			hmac_kernel<Sha256, true><<<grid, 256, 0, s>>>(base, offsets,
+			hmac_kernel<Sha256H, true><<<grid, 256, 0, s>>>(base, offsets,
 			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad);
 		} else {
-			hmac_kernel<Sha256, false><<<grid, 256, 0, s>>>(base, offsets,
+			hmac_kernel<Sha256H, false><<<grid, 256, 0, s>>>(base, offsets,
 			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad);
 		}
 	} else {

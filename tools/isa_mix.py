@@ -36,11 +36,11 @@ OUT = os.path.join(ROOT, "profiles", "isa_mix.json")
 
 # bench config -> mangled-name prefix of the kernel instance it launches
 KERNELS = {
-    "c2": "_ZN4net23dev12fixed_kernelINS0_6Sha256ELi0ELb1E",
+    "c2": "_ZN4net23dev12fixed_kernelINS0_7Sha256TILb1ELb1EEELi0ELb1E",
     "c4": "_ZN4net23dev12fixed_kernelINS0_6Sha512ELi0ELb1E",
-    "c3": "_ZN4net23dev10var_kernelINS0_6Sha256E",
-    "hmac": "_ZN4net23dev11hmac_kernelINS0_6Sha256ELb1E",
-    "hmac_mtu": "_ZN4net23dev11hmac_kernelINS0_6Sha256ELb0E",
+    "c3": "_ZN4net23dev10var_kernelINS0_7Sha256TILb0ELb0EEE",
+    "hmac": "_ZN4net23dev11hmac_kernelINS0_7Sha256TILb1ELb1EEELb1E",
+    "hmac_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha256TILb1ELb1EEELb0E",
     "hmac512": "_ZN4net23dev11hmac_kernelINS0_6Sha512ELb1E",
     "hmac512_mtu": "_ZN4net23dev11hmac_kernelINS0_6Sha512ELb0E",
 }
@@ -103,20 +103,31 @@ def kernel_body(lines, prefix):
 
 
 def innermost_loop(body):
-    """Lines of the innermost (deepest) loop: from its header label to the
-    branch back to it."""
+    """Lines of the innermost (deepest) loop: every basic block LLVM
+    annotates as belonging to it (`in Loop: Header=BBx_y`) plus the header
+    block itself, wherever the layout put them (rotated loops place the body
+    before the header)."""
+    blocks = []             # (label line index, annotation) per basic block
+    for i, ln in enumerate(body):
+        if re.match(r"^\.LBB\d+_\d+:", ln):
+            blocks.append(i)
+    blocks.append(len(body))
     best = None
     for i, ln in enumerate(body):
-        m = re.match(r"^(\.LBB\d+_\d+):.*Loop Header: Depth=(\d+)", ln)
+        m = re.match(r"^\.LBB(\d+_\d+):.*Loop Header: Depth=(\d+)", ln)
         if not m:
             continue
-        label, depth = m.group(1), int(m.group(2))
-        back = max(j for j, l2 in enumerate(body) if re.search(
-            r"s_c?branch\w*\s+" + re.escape(label) + r"$", l2.strip()))
-        n_valu = sum(1 for l2 in body[i:back + 1] if l2.strip().startswith("v_"))
+        tag, depth = m.group(1), int(m.group(2))
+        lines = []
+        for b0, b1 in zip(blocks, blocks[1:]):
+            head = body[b0]
+            if head.startswith(".LBB" + tag + ":") or (
+                    "Header=BB" + tag + " " in head + " "):
+                lines.extend(body[b0:b1])
+        n_valu = sum(1 for l2 in lines if l2.strip().startswith("v_"))
         key = (depth, n_valu)
         if best is None or key > best[0]:
-            best = (key, body[i:back + 1])
+            best = (key, lines)
     return best[1] if best else []
 
 

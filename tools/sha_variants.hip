@@ -11,6 +11,9 @@
 #include <algorithm>
 
 #define NBLK 17
+#ifndef WPE
+#define WPE 1
+#endif
 
 __device__ constexpr uint32_t K256[64] = {
 	0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu,
@@ -161,6 +164,116 @@ struct V5 {
 	}
 };
 
+
+// V6: each round / schedule word as one asm block, slow-class instructions
+// (alignbit, add3) grouped apart from fast-class ones (bitop3, add, lshr):
+// tests whether slow<->fast issue transitions cost cycles (valu_probe "mix").
+struct V6 {
+	template <int T> __device__ static void rnd(uint32_t (&s)[8], uint32_t w) {
+		uint32_t &a = s[(0 - T) & 7], &b = s[(1 - T) & 7], &c = s[(2 - T) & 7];
+		uint32_t &d = s[(3 - T) & 7], &e = s[(4 - T) & 7], &f = s[(5 - T) & 7];
+		uint32_t &g = s[(6 - T) & 7], &h = s[(7 - T) & 7];
+		uint32_t r1, r2, r3, r4, r5, r6, x, t1;
+		asm("v_alignbit_b32 %[r1], %[e], %[e], 6\n\t"
+		    "v_alignbit_b32 %[r2], %[e], %[e], 11\n\t"
+		    "v_alignbit_b32 %[r3], %[e], %[e], 25\n\t"
+		    "v_alignbit_b32 %[r4], %[a], %[a], 2\n\t"
+		    "v_alignbit_b32 %[r5], %[a], %[a], 13\n\t"
+		    "v_alignbit_b32 %[r6], %[a], %[a], 22\n\t"
+		    "v_add3_u32 %[x], %[h], %[k], %[w]\n\t"
+		    "v_bitop3_b32 %[r1], %[r1], %[r2], %[r3] bitop3:0x96\n\t"
+		    "v_bitop3_b32 %[r2], %[e], %[f], %[g] bitop3:0xca\n\t"
+		    "v_bitop3_b32 %[r4], %[r4], %[r5], %[r6] bitop3:0x96\n\t"
+		    "v_bitop3_b32 %[r5], %[a], %[b], %[c] bitop3:0xe8\n\t"
+		    "v_add3_u32 %[t1], %[x], %[r1], %[r2]\n\t"
+		    "v_add3_u32 %[h], %[t1], %[r4], %[r5]\n\t"
+		    "v_add_u32 %[d], %[d], %[t1]"
+		    : [r1] "=&v"(r1), [r2] "=&v"(r2), [r3] "=&v"(r3), [r4] "=&v"(r4),
+		      [r5] "=&v"(r5), [r6] "=&v"(r6), [x] "=&v"(x), [t1] "=&v"(t1),
+		      [h] "+v"(h), [d] "+v"(d)
+		    : [a] "v"(a), [b] "v"(b), [c] "v"(c), [e] "v"(e), [f] "v"(f),
+		      [g] "v"(g), [k] "s"(K256[T]), [w] "v"(w));
+	}
+	template <int T> __device__ static uint32_t exp(uint32_t (&w)[16]) {
+		uint32_t x = w[(T - 15) & 15], y = w[(T - 2) & 15];
+		uint32_t r1, r2, r3, r4, r5, r6;
+		asm("v_alignbit_b32 %[r1], %[y], %[y], 17\n\t"
+		    "v_alignbit_b32 %[r2], %[y], %[y], 19\n\t"
+		    "v_alignbit_b32 %[r3], %[x], %[x], 7\n\t"
+		    "v_alignbit_b32 %[r4], %[x], %[x], 18\n\t"
+		    "v_lshrrev_b32 %[r5], 10, %[y]\n\t"
+		    "v_lshrrev_b32 %[r6], 3, %[x]\n\t"
+		    "v_bitop3_b32 %[r1], %[r1], %[r2], %[r5] bitop3:0x96\n\t"
+		    "v_bitop3_b32 %[r3], %[r3], %[r4], %[r6] bitop3:0x96\n\t"
+		    "v_add3_u32 %[w16], %[w16], %[r1], %[w7]\n\t"
+		    "v_add_u32 %[w16], %[w16], %[r3]"
+		    : [r1] "=&v"(r1), [r2] "=&v"(r2), [r3] "=&v"(r3), [r4] "=&v"(r4),
+		      [r5] "=&v"(r5), [r6] "=&v"(r6), [w16] "+v"(w[T & 15])
+		    : [x] "v"(x), [y] "v"(y), [w7] "v"(w[(T - 7) & 15]));
+		return w[T & 15];
+	}
+};
+
+// V7: V6 order but interleaved slow/fast as much as dependencies allow
+struct V7 {
+	template <int T> __device__ static void rnd(uint32_t (&s)[8], uint32_t w) {
+		uint32_t &a = s[(0 - T) & 7], &b = s[(1 - T) & 7], &c = s[(2 - T) & 7];
+		uint32_t &d = s[(3 - T) & 7], &e = s[(4 - T) & 7], &f = s[(5 - T) & 7];
+		uint32_t &g = s[(6 - T) & 7], &h = s[(7 - T) & 7];
+		uint32_t r1, r2, r3, r4, r5, r6, x, t1;
+		asm("v_alignbit_b32 %[r1], %[e], %[e], 6\n\t"
+		    "v_bitop3_b32 %[r6], %[e], %[f], %[g] bitop3:0xca\n\t"
+		    "v_alignbit_b32 %[r2], %[e], %[e], 11\n\t"
+		    "v_bitop3_b32 %[r5], %[a], %[b], %[c] bitop3:0xe8\n\t"
+		    "v_alignbit_b32 %[r3], %[e], %[e], 25\n\t"
+		    "v_alignbit_b32 %[r4], %[a], %[a], 2\n\t"
+		    "v_bitop3_b32 %[r1], %[r1], %[r2], %[r3] bitop3:0x96\n\t"
+		    "v_alignbit_b32 %[r2], %[a], %[a], 13\n\t"
+		    "v_alignbit_b32 %[r3], %[a], %[a], 22\n\t"
+		    "v_add3_u32 %[x], %[h], %[k], %[w]\n\t"
+		    "v_bitop3_b32 %[r4], %[r4], %[r2], %[r3] bitop3:0x96\n\t"
+		    "v_add3_u32 %[t1], %[x], %[r1], %[r6]\n\t"
+		    "v_add_u32 %[d], %[d], %[t1]\n\t"
+		    "v_add3_u32 %[h], %[t1], %[r4], %[r5]"
+		    : [r1] "=&v"(r1), [r2] "=&v"(r2), [r3] "=&v"(r3), [r4] "=&v"(r4),
+		      [r5] "=&v"(r5), [r6] "=&v"(r6), [x] "=&v"(x), [t1] "=&v"(t1),
+		      [h] "+v"(h), [d] "+v"(d)
+		    : [a] "v"(a), [b] "v"(b), [c] "v"(c), [e] "v"(e), [f] "v"(f),
+		      [g] "v"(g), [k] "s"(K256[T]), [w] "v"(w));
+	}
+	template <int T> __device__ static uint32_t exp(uint32_t (&w)[16]) { return V6::exp<T>(w); }
+};
+
+// V8: builtins, V6's order written in the source; V9: V8 + a scheduling
+// barrier after every round (no inline asm, so no hazard s_nops)
+template <bool FENCE>
+struct V8T {
+	template <int T> __device__ static void rnd(uint32_t (&s)[8], uint32_t w) {
+		uint32_t &a = s[(0 - T) & 7], &b = s[(1 - T) & 7], &c = s[(2 - T) & 7];
+		uint32_t &d = s[(3 - T) & 7], &e = s[(4 - T) & 7], &f = s[(5 - T) & 7];
+		uint32_t &g = s[(6 - T) & 7], &h = s[(7 - T) & 7];
+		uint32_t r1 = rot_ab(e, 6), r2 = rot_ab(e, 11), r3 = rot_ab(e, 25);
+		uint32_t r4 = rot_ab(a, 2), r5 = rot_ab(a, 13), r6 = rot_ab(a, 22);
+		uint32_t x = h + K256[T] + w;
+		uint32_t s1 = x3_b3(r1, r2, r3), ch = ch_b3(e, f, g);
+		uint32_t s0 = x3_b3(r4, r5, r6), mj = mj_b3(a, b, c);
+		uint32_t t1 = x + s1 + ch;
+		h = t1 + s0 + mj;
+		d += t1;
+		if (FENCE)
+			__builtin_amdgcn_sched_barrier(0);
+	}
+	template <int T> __device__ static uint32_t exp(uint32_t (&w)[16]) {
+		uint32_t x = w[(T - 15) & 15], y = w[(T - 2) & 15];
+		uint32_t r1 = rot_ab(y, 17), r2 = rot_ab(y, 19), r3 = rot_ab(x, 7), r4 = rot_ab(x, 18);
+		uint32_t s1 = x3_b3(r1, r2, y >> 10), s0 = x3_b3(r3, r4, x >> 3);
+		w[T & 15] = w[T & 15] + s1 + w[(T - 7) & 15] + s0;
+		return w[T & 15];
+	}
+};
+typedef V8T<false> V8;
+typedef V8T<true> V9;
+
 template <class V, int T>
 struct R {
 	__device__ __forceinline__ static void run(uint32_t (&s)[8], uint32_t (&w)[16]) {
@@ -173,7 +286,7 @@ template <class V>
 struct R<V, 64> { __device__ __forceinline__ static void run(uint32_t (&)[8], uint32_t (&)[16]) {} };
 
 template <class V>
-__global__ __launch_bounds__(256) void kern(uint32_t *out, uint32_t seed)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void kern(uint32_t *out, uint32_t seed)
 {
 	uint32_t st[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
 	    0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
@@ -217,11 +330,13 @@ int main()
 	const int blocks = 4096;  // 16384 waves
 	const size_t n = (size_t)blocks * 256 * 8;
 	uint32_t *out;
-	(void)hipMalloc(&out, n * 4 * 6);
+	(void)hipMalloc(&out, n * 4 * 10);
 	std::vector<uint32_t> ref(n), got(n);
 	const char *names[] = {"V0 builtins (shipped)", "V1 VOP2 adds+xor, K literal", "V2 bitop3+add3, K literal",
-	    "V3 VOP2 logic Ch/Maj", "V4 shift rotations", "V5 bitop3 + VOP2 adds"};
-	float best[6] = {1e9, 1e9, 1e9, 1e9, 1e9, 1e9};
+	    "V3 VOP2 logic Ch/Maj", "V4 shift rotations", "V5 bitop3 + VOP2 adds",
+	    "V6 asm rounds, slow/fast grouped", "V7 asm rounds, slow/fast interleaved",
+	    "V8 builtins in V6 order", "V9 V8 + sched_barrier per round"};
+	float best[10] = {1e9, 1e9, 1e9, 1e9, 1e9, 1e9, 1e9, 1e9, 1e9, 1e9};
 	for (int round = 0; round < 3; round++) {
 		best[0] = std::min(best[0], timeit<V0>(out + 0 * n, blocks));
 		best[1] = std::min(best[1], timeit<V1>(out + 1 * n, blocks));
@@ -229,15 +344,19 @@ int main()
 		best[3] = std::min(best[3], timeit<V3>(out + 3 * n, blocks));
 		best[4] = std::min(best[4], timeit<V4>(out + 4 * n, blocks));
 		best[5] = std::min(best[5], timeit<V5>(out + 5 * n, blocks));
+		best[6] = std::min(best[6], timeit<V6>(out + 6 * n, blocks));
+		best[7] = std::min(best[7], timeit<V7>(out + 7 * n, blocks));
+		best[8] = std::min(best[8], timeit<V8>(out + 8 * n, blocks));
+		best[9] = std::min(best[9], timeit<V9>(out + 9 * n, blocks));
 	}
 	(void)hipMemcpy(ref.data(), out, n * 4, hipMemcpyDeviceToHost);
 	printf("{\"blocks_per_lane\": %d, \"waves\": %d, \"variants\": [\n", NBLK, blocks * 4);
-	for (int v = 0; v < 6; v++) {
+	for (int v = 0; v < 10; v++) {
 		(void)hipMemcpy(got.data(), out + v * n, n * 4, hipMemcpyDeviceToHost);
 		bool same = got == ref;
 		double per_block_ns = best[v] * 1e6 / ((double)blocks * 256 * NBLK);
 		printf("  {\"variant\": \"%s\", \"ms\": %.4f, \"same_as_V0\": %s, \"ps_per_lane_block\": %.3f}%s\n",
-		    names[v], best[v], same ? "true" : "false", per_block_ns * 1e3, v == 5 ? "" : ",");
+		    names[v], best[v], same ? "true" : "false", per_block_ns * 1e3, v == 9 ? "" : ",");
 	}
 	printf("]}\n");
 	return 0;

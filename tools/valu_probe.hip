@@ -65,7 +65,15 @@
 	if (K == 41) { if (c & 1) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(r[c]) : "v"(b), "v"(d)); \
 	               else asm volatile("v_add_u32 %0, %0, %1" : "+v"(r[c]) : "v"(b)); } \
 	if (K == 42) asm volatile("v_lshlrev_b32_e32 %0, %1, %0" : "+v"(r[c]) : "v"(b)); \
-	if (K == 43) asm volatile("v_mul_u32_u24_e32 %0, 0x80, %0" : "+v"(r[c]));
+	if (K == 43) asm volatile("v_mul_u32_u24_e32 %0, 0x80, %0" : "+v"(r[c])); \
+	if (K == 44) { if (c < 4) asm volatile("v_alignbit_b32 %0, %0, %0, 7" : "+v"(r[c])); \
+	               else asm volatile("v_xor_b32 %0, %0, %1" : "+v"(r[c]) : "v"(b)); } \
+	if (K == 45) { if (c < 4) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(r[c]) : "v"(b), "v"(d)); \
+	               else asm volatile("v_add_u32 %0, %0, %1" : "+v"(r[c]) : "v"(b)); } \
+	if (K == 46) asm volatile("v_bitop3_b32 %0, %0, %0, %0 bitop3:0x96" : "+v"(r[c])); \
+	if (K == 47) asm volatile("v_bitop3_b32 %0, %1, %2, %0 bitop3:0x96" : "+v"(r[c]) : "v"(r[(c + 1) % CHAINS]), "v"(r[(c + 2) % CHAINS])); \
+	if (K == 48) asm volatile("v_add3_u32 %0, %1, %2, %0" : "+v"(r[c]) : "v"(r[(c + 1) % CHAINS]), "v"(r[(c + 2) % CHAINS])); \
+	if (K == 49) asm volatile("v_alignbit_b32 %0, %1, %1, 7" : "=v"(r[c]) : "v"(r[(c + 3) % CHAINS]));
 
 static const char *kNames[] = {
 	"v_add_u32 (VOP2, v,v)", "v_xor_b32 (VOP2)", "v_lshrrev_b32 (VOP2, imm)",
@@ -84,8 +92,11 @@ static const char *kNames[] = {
 	"v_pk_add_f32", "v_add_f32", "v_and_b32", "v_not_b32", "v_sub_u32",
 	"mix alignbit|bitop3 1:1", "mix add3|add 1:1", "v_lshlrev_b32 v,v (VOP2 var shift)",
 	"v_mul_u32_u24 literal",
+	"grouped alignbit x4 | xor x4", "grouped add3 x4 | add x4",
+	"v_bitop3_b32 x,x,x", "v_bitop3_b32 chain-mixed srcs", "v_add3_u32 chain-mixed srcs",
+	"v_alignbit_b32 from other chain",
 };
-#define NK 44
+#define NK 50
 
 template <int K>
 __global__ __launch_bounds__(256) void probe(uint32_t *out, uint32_t seed)
