@@ -10,16 +10,22 @@ what each one costs the SIMD.  This tool:
   2. for each bench config's kernel, counts the VALU instructions of its
      innermost loop body (the block loop: >94 % of the instructions a C2/C4
      wave issues) by mnemonic and operand form,
-  3. prices them with the issue costs measured by tools/valu_probe.hip
-     (profiles/round1/valu_probe.json: SIMD cycles per wave64 instruction,
-     8 waves/SIMD, independent chains),
+  3. prices them: every instruction of a loop that mixes half-rate
+     (v_alignbit, v_add3, v_perm, v_lshl_add_u64, ...) and full-rate
+     (v_bitop3, v_add, v_xor, v_lshrrev, ...) instructions at the measured
+     cost of such a stream (profiles/round1/valu_bank_seq_probe.json, row
+     "mix: 3 rot + bitop3 (Sigma)": 3.95 SIMD cycles per wave64 instruction
+     at 2.4 GHz, 8 waves/SIMD).  The probe's sequence rows show why: in a
+     mixed stream every instruction issues at ~4 cycles, whatever its
+     class (S F S F 4.11, S F F F 4.09, 8 S then 8 F 3.87; pure full-rate
+     2.44, pure half-rate 4.21).  The additive price (each instruction at
+     its own pure-stream cost, profiles/round1/valu_probe.json) is kept
+     alongside as the optimistic bound,
   4. writes profiles/isa_mix.json: per config, the loop's instruction mix and
      its mean issue cost per VALU instruction (cycles).
 
 bench.py multiplies that mean by the launch's SQ_INSTS_VALU (rocprofv3) to
 get the launch's issue floor, and reports the measured launch against it.
-The model is additive (costs of a mixed stream add up); the probe's "mix"
-rows show it holds to within about +-10 % per pair, in both directions.
 """
 from __future__ import annotations
 
@@ -32,6 +38,10 @@ from collections import Counter
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ASM = os.path.join(ROOT, "ilias_net2_amd", "csrc", "build", "sha2_kernels.s")
 PROBE = os.path.join(ROOT, "profiles", "round1", "valu_probe.json")
+# explicit-register probe (tools/gen_bank_probe.py): VGPR banks, slow/fast
+# sequences and the Sigma-shaped mix
+SEQ_PROBE = os.path.join(ROOT, "profiles", "round1", "valu_bank_seq_probe.json")
+MIXED_ROW = "mix: 3 rot + bitop3 (Sigma), 3-bank"
 OUT = os.path.join(ROOT, "profiles", "isa_mix.json")
 
 # bench config -> mangled-name prefix of the kernel instance it launches
@@ -88,9 +98,12 @@ def cost_table(probe_path=PROBE):
         if r["waves_per_simd"] != 8 or r["op"] not in PROBE_ROWS:
             continue
         t[PROBE_ROWS[r["op"]]] = r["simd_cycles_per_wave_instr_at_2.4GHz"]
-    # bitop3: mean of the two truth tables measured (xor3 0x96, ch 0xca)
-    b3 = [r["simd_cycles_per_wave_instr_at_2.4GHz"] for r in rows
-          if r["waves_per_simd"] == 8 and r["op"].startswith("v_bitop3_b32")]
+    # bitop3: the explicit-register rows of the bank probe (2.5-2.6; the
+    # first probe's 3.6-3.8 came from its operand placement, not the op)
+    with open(SEQ_PROBE) as f:
+        seq = json.load(f)["results"]
+    b3 = [r["simd_cycles_per_wave_instr_at_2.4GHz"] for r in seq
+          if r["op"].startswith("v_bitop3_b32")]
     t[("v_bitop3_b32", "v")] = sum(b3) / len(b3)
     return t
 
@@ -160,6 +173,21 @@ def price(mn, form, table):
     return 4.3, "unprobed: slow-class cost assumed"
 
 
+def mixed_stream_cost(path=SEQ_PROBE):
+    """Issue cost per instruction of a stream that mixes half-rate
+    (v_alignbit, v_add3, ...) and full-rate (v_bitop3, v_add, ...) ops.
+
+    The sequence rows of the bank probe show that in such a stream every
+    instruction issues at ~4 cycles whatever its class (S F S F: 4.11,
+    S F F F: 4.09, 8 S then 8 F: 3.87), so the binding floor is the
+    instruction count times the cost of the round-shaped mix (three
+    rotates + one bitop3, 3.95)."""
+    with open(path) as f:
+        rows = json.load(f)["results"]
+    return next(r["simd_cycles_per_wave_instr_at_2.4GHz"] for r in rows
+                if r["op"] == MIXED_ROW)
+
+
 def analyse(lines, prefix, table):
     body = kernel_body(lines, prefix)
     loop = innermost_loop(body)
@@ -176,9 +204,18 @@ def analyse(lines, prefix, table):
         cyc += c * n
         rows.append({"instr": mn, "operands": form, "count": n,
                      "cycles_each": round(c, 3), "priced": how})
+    mixed = mixed_stream_cost()
+    kinds = {("fast" if table.get((r["instr"], r["operands"]), 4.3) < 3.0 else "slow")
+             for r in rows}
     return {"kernel": prefix, "loop_valu_instr": total_instr,
-            "loop_issue_cycles": round(cyc, 1),
-            "mean_issue_cycles_per_valu_instr": round(cyc / total_instr, 4) if total_instr else None,
+            # binding model: a mixed stream issues every instruction at the
+            # Sigma-shaped mix's cost (mixed_stream_cost)
+            "mean_issue_cycles_per_valu_instr": (mixed if kinds == {"fast", "slow"}
+                                                 else round(cyc / total_instr, 4)) if total_instr else None,
+            "model": "mixed-stream: instructions x %s (%s)" % (mixed, MIXED_ROW),
+            # optimistic: each instruction at its own pure-stream cost
+            "additive_issue_cycles": round(cyc, 1),
+            "additive_mean_cycles_per_valu_instr": round(cyc / total_instr, 4) if total_instr else None,
             "mix": rows}
 
 
@@ -193,6 +230,7 @@ def main():
     res = {"source": "tools/isa_mix.py over `make asm` output; costs from "
                      "profiles/round1/valu_probe.json (SIMD cycles per wave64 "
                      "instruction at 2.4 GHz, 8 waves/SIMD)",
+           "mixed_stream_source": SEQ_PROBE.replace(ROOT + "/", ""),
            "configs": {}}
     for cfg, prefix in KERNELS.items():
         res["configs"][cfg] = analyse(lines, prefix, table)
