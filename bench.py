@@ -288,9 +288,10 @@ def main():
                 "unit": "T wave64-VALU-instr/s",
                 "frac": round(rate / VALU_PEAK_WAVE_INSTR, 4),
                 # SIMD cycles between VALU issues, averaged over the launch:
-                # 2.0 = the nominal SIMD-32 rate; tools/valu_probe measured
-                # ~4.1 for v_alignbit/v_add3/v_perm and ~3.5 for v_bitop3,
-                # which make up >90% of the SHA rounds
+                # 2.0 = the nominal SIMD-32 rate, reached only by full-rate
+                # ops in a pure stream; v_alignbit/v_add3/v_perm are
+                # half-rate (4.2), and a stream mixing the two classes issues
+                # every instruction at ~4
                 "simd_cycles_per_valu_instr": round(clk * 1e9 * (launch_ms / 1e3) * 1024 / instr, 3),
                 "clock_ghz": round(clk, 3),
                 "instr_per_launch": instr,
@@ -298,15 +299,15 @@ def main():
         mix = load_isa_mix(args.config)
         if mix and mix.get("mean_issue_cycles_per_valu_instr"):
             # Issue floor: every VALU instruction of the launch priced at the
-            # mean measured cost of the block loop's mix (tools/isa_mix.py,
-            # probe costs normalised to 2.4 GHz like the probe itself).
+            # measured issue cost of a mixed half/full-rate stream
+            # (tools/isa_mix.py, probe cycles at 2.4 GHz like the probe).
             m = mix["mean_issue_cycles_per_valu_instr"]
             floor_ms = instr / 1024 * m / 2.4e9 * 1e3
             valu["issue_floor"] = {
                 "mean_cycles_per_valu_instr": m,
                 "floor_ms": round(floor_ms, 4),
                 "frac": round(floor_ms / launch_ms, 4),
-                "source": "profiles/isa_mix.json (loop mix) x profiles/round1/valu_probe.json (costs)"}
+                "source": "profiles/isa_mix.json (mixed-stream model) x profiles/round1/valu_bank_seq_probe.json (cost)"}
 
     line = {
         "metric": METRIC if args.config == "c2" else
