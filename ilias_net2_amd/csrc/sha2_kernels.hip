@@ -699,10 +699,21 @@ __device__ __forceinline__ uint32_t bin_of(uint32_t len, int blk_shift,
 }
 
 /* Packets per thread in the binning kernels: one workgroup bins a tile of
- * 256 x 16 = 4,096 packets, so the 2,048-entry LDS histogram is cleared
- * and flushed once per 4,096 packets. */
-#define NET2_BIN_ITEMS 16
+ * 256 x 8 = 2,048 packets, so the 2,048-entry LDS histogram is cleared and
+ * flushed once per 2,048 packets (512 workgroups per 1 M packets; 4 and 16
+ * items measured 1-2 % slower on C3, profiles/round1/binning_ab.txt). */
+#ifndef NET2_BIN_ITEMS
+#define NET2_BIN_ITEMS 8
+#endif
 #define NET2_BIN_TILE (256 * NET2_BIN_ITEMS)
+/*
+ * 1: no separate scan launch -- every scatter workgroup scans the 2,048-bin
+ * histogram itself (8 KiB, L2-resident) and claims its ranges from a zeroed
+ * per-bin counter; 0: count, scan (one workgroup), scatter.
+ */
+#ifndef NET2_BIN_FUSED
+#define NET2_BIN_FUSED 1
+#endif
 
 /*
  * Wave-aggregated LDS counter add: the lanes of a wave that carry the same
@@ -782,6 +793,42 @@ __global__ __launch_bounds__(1024) void bin_scan_kernel(
 }
 
 /*
+ * Exclusive prefix of the global histogram into LDS (NET2_BIN_FUSED): each
+ * of the 256 threads sums 8 consecutive bins, a shuffle scan per wave and
+ * the four wave totals give its offset.
+ */
+__device__ __forceinline__ void hist_prefix_lds(const uint32_t *__restrict__ hist,
+    uint32_t *pre)
+{
+	__shared__ uint32_t wsum[4];
+	constexpr int PER = NET2_SHA2_NBINS / 256;
+	const int lane = (int)__lane_id(), wave = (int)(threadIdx.x / 64);
+	uint32_t v[PER], s = 0;
+#pragma unroll
+	for (int j = 0; j < PER; j++) {
+		const uint32_t t = hist[threadIdx.x * PER + j];
+		v[j] = s;
+		s += t;
+	}
+	uint32_t x = s;
+#pragma unroll
+	for (int off = 1; off < 64; off <<= 1) {
+		const uint32_t y = __shfl_up(x, off);
+		if (lane >= off)
+			x += y;
+	}
+	if (lane == 63)
+		wsum[wave] = x;
+	__syncthreads();
+	uint32_t base = x - s;
+	for (int w = 0; w < wave; w++)
+		base += wsum[w];
+#pragma unroll
+	for (int j = 0; j < PER; j++)
+		pre[threadIdx.x * PER + j] = base + v[j];
+}
+
+/*
  * Scatter packet indices to their bin.  Each block ranks its own packets
  * per bin in LDS, claims one range per touched bin with a single global
  * atomic, then writes perm[].  Order inside a bin is unspecified; digests
@@ -789,12 +836,15 @@ __global__ __launch_bounds__(1024) void bin_scan_kernel(
  */
 __global__ __launch_bounds__(256) void bin_scatter_kernel(
     const uint32_t *__restrict__ lens, uint64_t n, int blk_shift,
-    int lenbytes, uint32_t *__restrict__ cursor, uint32_t *__restrict__ perm)
+    int lenbytes, const uint32_t *__restrict__ hist,
+    uint32_t *__restrict__ cursor, uint32_t *__restrict__ perm)
 {
 	__shared__ uint32_t cnt[NET2_SHA2_NBINS];
 	__shared__ uint32_t basep[NET2_SHA2_NBINS];
 	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
 		cnt[b] = 0;
+	if (NET2_BIN_FUSED)
+		hist_prefix_lds(hist, basep);
 	__syncthreads();
 	const uint64_t i0 = (uint64_t)blockIdx.x * NET2_BIN_TILE + threadIdx.x;
 	uint32_t bin[NET2_BIN_ITEMS], rank[NET2_BIN_ITEMS];
@@ -809,7 +859,8 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(
 	__syncthreads();
 	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
 		if (cnt[b] != 0)
-			basep[b] = atomicAdd(&cursor[b], cnt[b]);
+			basep[b] = (NET2_BIN_FUSED ? basep[b] : 0) +
+			    atomicAdd(&cursor[b], cnt[b]);
 	__syncthreads();
 #pragma unroll
 	for (int k = 0; k < NET2_BIN_ITEMS; k++) {
@@ -928,15 +979,17 @@ hipError_t net2_bin_order(int alg, const uint32_t *lens, uint64_t n,
 	uint32_t *hist = ws;
 	uint32_t *cursor = ws + NET2_SHA2_NBINS;
 	uint32_t *perm = ws + 2 * NET2_SHA2_NBINS;
-	hipError_t e = hipMemsetAsync(hist, 0, NET2_SHA2_NBINS * sizeof(uint32_t),
-	    s);
+	/* fused: cursor holds per-bin claim counters, zeroed with hist */
+	hipError_t e = hipMemsetAsync(hist, 0, (NET2_BIN_FUSED ? 2 : 1) *
+	    NET2_SHA2_NBINS * sizeof(uint32_t), s);
 	if (e != hipSuccess)
 		return e;
 	const unsigned g = (unsigned)((n + NET2_BIN_TILE - 1) / NET2_BIN_TILE);
 	bin_count_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift, lenbytes, hist);
-	bin_scan_kernel<<<1, 1024, 0, s>>>(hist, cursor);
-	bin_scatter_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift, lenbytes, cursor,
-	    perm);
+	if (!NET2_BIN_FUSED)
+		bin_scan_kernel<<<1, 1024, 0, s>>>(hist, cursor);
+	bin_scatter_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift, lenbytes, hist,
+	    cursor, perm);
 	return hipGetLastError();
 }
 
