@@ -73,11 +73,15 @@ struct Sha256T {
 #ifndef NET2_ABSORB_U2
 #define NET2_ABSORB_U2 1
 #endif
+/* 1: the U2 block loop loads both blocks of a trip together (see absorb) */
+#ifndef NET2_PAIR_LOAD
+#define NET2_PAIR_LOAD 0
+#endif
 #ifndef NET2_VAR_ASM
 #define NET2_VAR_ASM 0
 #endif
 #ifndef NET2_VAR_U2
-#define NET2_VAR_U2 0
+#define NET2_VAR_U2 1
 #endif
 #ifndef NET2_HMAC_ASM
 #define NET2_HMAC_ASM 1
@@ -278,7 +282,37 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 	constexpr int NW32 = H::NW32;
 	const uint32_t nfull = len / H::BLOCK;
 
-	if (PREFETCH && H::U2) {
+	if (PREFETCH && H::U2 && NET2_PAIR_LOAD) {
+		/*
+		 * Both blocks of a trip -- one 128-byte line of an aligned packet --
+		 * requested together at the top of the trip, no prefetch: the
+		 * other waves of the SIMD cover the wait.  With a one-block-ahead
+		 * prefetch the second half of a line was requested one
+		 * compression (~20 us) after the first, long enough for many lines
+		 * to leave the 4 MB L2 of the XCD in between and be fetched again.
+		 */
+		uint32_t k = 0;
+		for (; k + 2 <= nfull; k += 2) {
+			const uint8_t *bp = p + (size_t)k * H::BLOCK;
+			Raw<NW32> ra, rb;
+			issue_block<NW32, AMODE>(bp, ra);
+			issue_block<NW32, AMODE>(bp + H::BLOCK, rb);
+			uint32_t w[NW32];
+			finish_block<NW32, AMODE>(bp, ra, w);
+			H::compress(st, w);
+			uint32_t w2[NW32];
+			finish_block<NW32, AMODE>(bp + H::BLOCK, rb, w2);
+			H::compress(st, w2);
+		}
+		if (k < nfull) {
+			const uint8_t *bp = p + (size_t)k * H::BLOCK;
+			Raw<NW32> ra;
+			issue_block<NW32, AMODE>(bp, ra);
+			uint32_t w[NW32];
+			finish_block<NW32, AMODE>(bp, ra, w);
+			H::compress(st, w);
+		}
+	} else if (PREFETCH && H::U2) {
 		/*
 		 * Two blocks per trip with the buffers swapping roles, so the
 		 * prefetched block is consumed where it landed (a one-block loop
