@@ -373,7 +373,9 @@ int run_device_slice(size_t didx, int alg, const uint8_t *base,
 	return rc ? rc : rc2 ? rc2 : rc3;
 }
 
-/* Single message, gathered from iovecs, on the first device. */
+/* Single message, gathered from iovecs, on the calling thread's current
+ * device when it is a usable one (one process per GPU stays on its GPU),
+ * else on the first. */
 int hash_small(int alg, const uint8_t *key, size_t keylen,
     const struct iovec *iov, size_t iovcnt, uint8_t *out)
 {
@@ -382,11 +384,21 @@ int hash_small(int alg, const uint8_t *key, size_t keylen,
 		total += iov[i].iov_len;
 	if (total > UINT32_MAX)
 		return EINVAL;
-	DeviceCtx *c = ctx_for(0);
-	std::lock_guard<std::mutex> g(c->small_mu);
 	int prev = -1;
 	(void)hipGetDevice(&prev);
-	HIP_TRY(hipSetDevice(devices()[0]));
+	const std::vector<int> &dv = devices();
+	size_t didx = 0;
+	for (size_t d = 0; d < dv.size(); d++)
+		if (dv[d] == prev)
+			didx = d;
+	DeviceCtx *c = ctx_for(didx);
+	std::lock_guard<std::mutex> g(c->small_mu);
+	HIP_TRY(hipSetDevice(dv[didx]));
+	/* the caller's current device is restored on every return below */
+	struct Restore {
+		int dev;
+		~Restore() { if (dev >= 0) (void)hipSetDevice(dev); }
+	} restore = { prev };
 	Slot &s = c->small;
 	int rc = s.reserve(total, 1);
 	if (rc != 0)
@@ -411,8 +423,6 @@ int hash_small(int alg, const uint8_t *key, size_t keylen,
 	    s.stream));
 	HIP_TRY(hipStreamSynchronize(s.stream));
 	memcpy(out, s.h_dig, dl);
-	if (prev >= 0)
-		(void)hipSetDevice(prev);
 	return 0;
 }
 
