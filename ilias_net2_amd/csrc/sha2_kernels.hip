@@ -733,11 +733,13 @@ __device__ __forceinline__ uint32_t bin_of(uint32_t len, int blk_shift,
 }
 
 /* Packets per thread in the binning kernels: one workgroup bins a tile of
- * 256 x 8 = 2,048 packets, so the 2,048-entry LDS histogram is cleared and
- * flushed once per 2,048 packets (512 workgroups per 1 M packets; 4 and 16
- * items measured 1-2 % slower on C3, profiles/round1/binning_ab.txt). */
+ * 256 x 16 = 4,096 packets (256 workgroups per 1 M packets).  Every
+ * workgroup pays a fixed cost (clearing and flushing the 2,048-bin LDS
+ * histogram, the scatter's histogram scan, its global atomics), so fewer,
+ * larger tiles win down to 4,096 packets; 2,048 and 8,192 measured slower
+ * (profiles/round1/binning_time_ab.txt). */
 #ifndef NET2_BIN_ITEMS
-#define NET2_BIN_ITEMS 8
+#define NET2_BIN_ITEMS 16
 #endif
 #define NET2_BIN_TILE (256 * NET2_BIN_ITEMS)
 /*
@@ -755,9 +757,19 @@ __device__ __forceinline__ uint32_t bin_of(uint32_t len, int blk_shift,
  * batch puts 3 keys in a wave: 3 LDS atomics instead of 64).  Returns the
  * counter's value before the group's add plus this lane's rank in its group.
  */
+/* 0: one LDS atomic per lane (shipped: binning 25 -> 16 us per 1 M packets
+ * with 4,096-packet tiles, profiles/round1/binning_time_ab.txt); 1: the
+ * wave-aggregated loop below (ballot per distinct key, one atomic each). */
+#ifndef NET2_BIN_WAVEAGG
+#define NET2_BIN_WAVEAGG 0
+#endif
 __device__ __forceinline__ uint32_t wave_rank_add(uint32_t *ctr, uint32_t key,
     bool active)
 {
+	if (!NET2_BIN_WAVEAGG) {
+		/* one LDS atomic per lane; the LDS serialises equal addresses */
+		return active ? atomicAdd(&ctr[key], 1u) : 0u;
+	}
 	uint64_t todo = __ballot(active);
 	const uint64_t below = __lanemask_lt();
 	const int lane = (int)__lane_id();
@@ -777,6 +789,21 @@ __device__ __forceinline__ uint32_t wave_rank_add(uint32_t *ctr, uint32_t key,
 	return rank;
 }
 
+/*
+ * A thread's NET2_BIN_ITEMS lengths, all loads issued before any is used:
+ * behind the data-dependent loop of wave_rank_add the compiler would
+ * otherwise wait out one memory latency per item.
+ */
+__device__ __forceinline__ void load_lens(const uint32_t *__restrict__ lens,
+    uint64_t n, uint64_t i0, uint32_t (&len)[NET2_BIN_ITEMS])
+{
+#pragma unroll
+	for (int k = 0; k < NET2_BIN_ITEMS; k++) {
+		const uint64_t i = i0 + (uint64_t)k * 256;
+		len[k] = i < n ? lens[i] : 0u;
+	}
+}
+
 __global__ __launch_bounds__(256) void bin_count_kernel(
     const uint32_t *__restrict__ lens, uint64_t n, int blk_shift,
     int lenbytes, uint32_t *__restrict__ hist)
@@ -786,11 +813,12 @@ __global__ __launch_bounds__(256) void bin_count_kernel(
 		lh[b] = 0;
 	__syncthreads();
 	const uint64_t i0 = (uint64_t)blockIdx.x * NET2_BIN_TILE + threadIdx.x;
+	uint32_t len[NET2_BIN_ITEMS];
+	load_lens(lens, n, i0, len);
 #pragma unroll
 	for (int k = 0; k < NET2_BIN_ITEMS; k++) {
-		const uint64_t i = i0 + (uint64_t)k * 256;
-		const bool live = i < n;
-		const uint32_t bin = live ? bin_of(lens[i], blk_shift, lenbytes,
+		const bool live = i0 + (uint64_t)k * 256 < n;
+		const uint32_t bin = live ? bin_of(len[k], blk_shift, lenbytes,
 		    NET2_SHA2_NBINS) : 0;
 		(void)wave_rank_add(lh, bin, live);
 	}
@@ -882,11 +910,11 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(
 	__syncthreads();
 	const uint64_t i0 = (uint64_t)blockIdx.x * NET2_BIN_TILE + threadIdx.x;
 	uint32_t bin[NET2_BIN_ITEMS], rank[NET2_BIN_ITEMS];
+	load_lens(lens, n, i0, bin);
 #pragma unroll
 	for (int k = 0; k < NET2_BIN_ITEMS; k++) {
-		const uint64_t i = i0 + (uint64_t)k * 256;
-		const bool live = i < n;
-		bin[k] = live ? bin_of(lens[i], blk_shift, lenbytes,
+		const bool live = i0 + (uint64_t)k * 256 < n;
+		bin[k] = live ? bin_of(bin[k], blk_shift, lenbytes,
 		    NET2_SHA2_NBINS) : 0;
 		rank[k] = wave_rank_add(cnt, bin[k], live);
 	}
