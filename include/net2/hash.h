@@ -58,7 +58,9 @@ int net2_hash_getkeylen(int alg);
  * digest (net2_hash_gethashlen(alg) bytes) to out, which holds outlen
  * bytes.  Returns 0, EINVAL (bad row, key length or outlen; an unkeyed row
  * given a key: hash-openssl.cc:199-200,227-228), ENOMEM, ENODEV or EIO.
- * nil writes nothing and returns 0.
+ * nil writes nothing and returns 0.  Runs on the calling thread's current
+ * HIP device if it is a gfx950, else on the first gfx950; the current
+ * device is unchanged on return.
  */
 int net2_hashctx_hashiov(int alg, const void *key, size_t keylen,
     const struct iovec *iov, size_t iovcnt, void *out, size_t outlen);
