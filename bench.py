@@ -46,6 +46,11 @@ CONFIGS = {
                     workload="1M x 1 KiB packets, HMAC-SHA512, device-resident (8f row 1)"),
     "hmac512_mtu": dict(alg=6, kind="mixed", n=1 << 20, length=None,
                         workload="1M x mixed {64,512,1500} B datagrams, HMAC-SHA512, binned (8f row 1)"),
+    # RX side of the datagram authenticator: each {64,512,1500} B datagram
+    # is a 32-byte HMAC field || message (types/packet.n2t:226-257); one
+    # result byte per datagram
+    "hmac_verify_mtu": dict(alg=4, kind="dgram_verify", n=1 << 20, length=None,
+                            workload="1M x mixed {64,512,1500} B datagrams, HMAC-SHA256 verify (hash field || message), binned (8f row 1, RX)"),
     "ph_iv": dict(alg=1, kind="ph_iv", n=1 << 20, length=16,
                   workload="1M packet headers -> 16-byte IVs, net2_ph_to_iv_dev (8f row 3)"),
 }
@@ -202,15 +207,25 @@ def main():
     cfg = CONFIGS[args.config]
     inp = make_inputs(cfg, dev, seed=2 + rank)
     n, alg = inp["n"], cfg["alg"]
-    dlen = cfg["length"] if cfg["kind"] == "ph_iv" else DLEN[alg]
+    dlen = cfg["length"] if cfg["kind"] == "ph_iv" else \
+        1 if cfg["kind"] == "dgram_verify" else DLEN[alg]
     out = torch.empty((n, dlen), dtype=torch.uint8, device=dev)
-    ws_buf = batch.var_workspace(n, dev) if cfg["kind"] == "mixed" else None
+    ws_buf = batch.var_workspace(n, dev) if cfg["kind"] in ("mixed", "dgram_verify") else None
+    kbuf = HMAC_KEY[:DLEN[alg]] if alg >= 4 else b""
+    if cfg["kind"] == "dgram_verify":
+        # sign once (untimed) so every datagram verifies
+        batch.hmac_sign_dev(alg, kbuf, inp["data"], inp["offs"], inp["lens"])
     stream = torch.cuda.current_stream(dev)
     L = _lib.lib()
-    kbuf = HMAC_KEY[:DLEN[alg]] if alg >= 4 else b""
 
     def step():
-        if cfg["kind"] == "ph_iv":
+        if cfg["kind"] == "dgram_verify":
+            _lib.check(L.net2_hmac_verify_dev(
+                alg, kbuf, len(kbuf), inp["data"].data_ptr(),
+                inp["offs"].data_ptr(), inp["lens"].data_ptr(), n,
+                out.data_ptr(), ws_buf.data_ptr(), ws_buf.numel() * 4,
+                stream.cuda_stream))
+        elif cfg["kind"] == "ph_iv":
             _lib.check(L.net2_ph_to_iv_dev(inp["seq"].data_ptr(), inp["flags"].data_ptr(),
                                            n, cfg["length"], out.data_ptr(),
                                            stream.cuda_stream))
@@ -270,7 +285,7 @@ def main():
     # Roofline of the dominant kernel: algorithmic bytes = payload read +
     # digests written (+ 12 B/packet offsets+lens for the mixed layout),
     # per launch, over the event-timed launch duration.
-    per_launch = inp["payload"] + n * dlen + (12 * n if cfg["kind"] == "mixed" else 0)
+    per_launch = inp["payload"] + n * dlen + (12 * n if cfg["kind"] in ("mixed", "dgram_verify") else 0)
     achieved = per_launch / (launch_ms / 1e3) / 1e9
     pmc = load_pmc(args.config)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -312,6 +327,7 @@ def main():
     line = {
         "metric": METRIC if args.config == "c2" else
         ("SHA-256 IVs/s, " if cfg["kind"] == "ph_iv" else
+         f"{ALG_NAMES[alg]} datagrams verified/s, " if cfg["kind"] == "dgram_verify" else
          f"{ALG_NAMES[alg]} digests/s, ") + cfg["workload"],
         "value": round(value, 1), "unit": "digests/s", "n_gpus": ws,
         "steps": args.steps, "warmup": args.warmup,

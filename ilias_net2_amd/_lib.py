@@ -66,6 +66,14 @@ SIGNATURES = {
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
         ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
         ctypes.c_void_p]),
+    "net2_hmac_sign_dev": (ctypes.c_int, [
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+        ctypes.c_size_t, ctypes.c_void_p]),
+    "net2_hmac_verify_dev": (ctypes.c_int, [
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
     "net2_ph_to_iv": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t,
                                       ctypes.c_void_p]),
     "net2_ph_to_iv_dev": (ctypes.c_int, [

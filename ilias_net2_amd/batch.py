@@ -149,3 +149,49 @@ def hmac_dev(alg: int, key: bytes, data, stride: int = 0, length: int = 0,
     if ws_ptr is not None:
         torch.cuda.current_stream(data.device).synchronize()
     return out
+
+
+def _dgram_args(alg, key, data, offsets, lens, binned):
+    import torch
+    _need(data, torch.uint8, "data")
+    _need(offsets, torch.int64, "offsets")
+    _need(lens, torch.int32, "lens")
+    n = int(offsets.numel())
+    kb = ctypes.create_string_buffer(bytes(key), max(len(key), 1))
+    ws = var_workspace(n, data.device) if binned and n else None
+    return n, kb, ws
+
+
+def hmac_sign_dev(alg: int, key: bytes, data, offsets, lens,
+                  binned: bool = True, stream=None):
+    """TX side of the per-datagram authenticator (types/packet.n2t:410-427):
+    datagram i = data[offsets[i] : offsets[i] + lens[i]] is hash field ||
+    message; the first hashlen bytes receive HMAC(key, message), in place."""
+    n, kb, ws = _dgram_args(alg, key, data, offsets, lens, binned)
+    rc = _lib.lib().net2_hmac_sign_dev(
+        alg, kb, len(key), data.data_ptr(), offsets.data_ptr(),
+        lens.data_ptr(), n, None if ws is None else ws.data_ptr(),
+        0 if ws is None else ws.numel() * 4, _stream_ptr(stream))
+    check(rc, "net2_hmac_sign_dev")
+    if ws is not None:
+        import torch
+        torch.cuda.current_stream(data.device).synchronize()
+    return data
+
+
+def hmac_verify_dev(alg: int, key: bytes, data, offsets, lens,
+                    binned: bool = True, stream=None):
+    """RX side (types/packet.n2t:226-257): uint8 per datagram, 0 if its hash
+    field equals HMAC(key, message), 1 if not, 2 if shorter than hashlen."""
+    import torch
+    n, kb, ws = _dgram_args(alg, key, data, offsets, lens, binned)
+    res = torch.empty((n,), dtype=torch.uint8, device=data.device)
+    rc = _lib.lib().net2_hmac_verify_dev(
+        alg, kb, len(key), data.data_ptr(), offsets.data_ptr(),
+        lens.data_ptr(), n, res.data_ptr(),
+        None if ws is None else ws.data_ptr(),
+        0 if ws is None else ws.numel() * 4, _stream_ptr(stream))
+    check(rc, "net2_hmac_verify_dev")
+    if ws is not None:
+        torch.cuda.current_stream(data.device).synchronize()
+    return res

@@ -602,8 +602,23 @@ __device__ __forceinline__ void hmac_lane(const uint8_t *p, uint32_t len,
  * PADCONST: fixed layout with fixed_len % BLOCK == 0, so the inner pad
  * block (bit count = (BLOCK + fixed_len) * 8) is the same for every lane
  * and its K + W schedule comes precomputed in pad, as in fixed_kernel.
+ *
+ * MODE (variable layout only for SIGN / VERIFY): datagram i is
+ * base[offsets[i] .. + lens[i]) = hash field (dlen bytes) || message, the
+ * wire order of net2_packet_encode (the hash is prepended,
+ * types/packet.n2t:417-427) and net2_packet_decode (it is removed first,
+ * :236-244).
+ *   HMAC_DIGESTS: digest of the whole packet to out + i * dlen;
+ *   HMAC_SIGN:    digest of the message into the datagram's hash field
+ *                 (out == base, writable); datagrams shorter than dlen are
+ *                 left untouched;
+ *   HMAC_VERIFY:  out[i] = 0 if the hash field equals the digest of the
+ *                 message (the net2_buffer_cmp of :254), 1 if it does not,
+ *                 2 if the datagram is shorter than dlen (:240-244).
  */
-template <class H, bool PADCONST>
+enum { HMAC_DIGESTS = 0, HMAC_SIGN = 1, HMAC_VERIFY = 2 };
+
+template <class H, bool PADCONST, int MODE = HMAC_DIGESTS>
 __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ base,
     const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
     const uint32_t *__restrict__ perm, uint64_t stride, uint32_t fixed_len,
@@ -652,6 +667,12 @@ __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ b
 		p = base + (live ? i * stride : 0);
 		len = live ? fixed_len : 0;
 	}
+	const uint8_t *field = p;	/* SIGN / VERIFY: the hash field */
+	const bool short_dgram = MODE != HMAC_DIGESTS && len < dlen;
+	if (MODE != HMAC_DIGESTS) {
+		p += short_dgram ? 0 : dlen;
+		len = short_dgram ? 0 : len - dlen;
+	}
 	typename H::State st;
 	const uintptr_t pa = reinterpret_cast<uintptr_t>(p);
 	const int amode = __all((pa & 15) == 0) ? AMODE_A16 :
@@ -662,12 +683,24 @@ __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ b
 		return;
 	uint32_t o[16];
 	H::out_words(st, o, is384);
+	if (MODE == HMAC_VERIFY) {
+		/* o[] holds the digest bytes little-endian per word, the order
+		 * store_digest writes them in */
+		uint32_t diff = 0;
+		for (uint32_t j = 0; j < dlen && !short_dgram; j++)
+			diff |= field[j] ^ ((o[j >> 2] >> (8 * (j & 3))) & 0xffu);
+		out[i] = short_dgram ? 2 : diff != 0;
+		return;
+	}
+	uint8_t *dst = MODE == HMAC_SIGN ? out + (field - base) : out + i * dlen;
+	if (MODE == HMAC_SIGN && short_dgram)
+		return;
 	if (dlen == 48)
-		store_digest<48>(out + i * 48, o);
+		store_digest<48>(dst, o);
 	else if (dlen == 32)
-		store_digest<32>(out + i * 32, o);
+		store_digest<32>(dst, o);
 	else
-		store_digest<64>(out + i * 64, o);
+		store_digest<64>(dst, o);
 }
 
 /* ---- packet-header IV derivation (types/packet.n2t:100-158) ---------------- */
@@ -1080,11 +1113,30 @@ hipError_t net2_launch_var(int alg, const uint8_t *base,
 		    lens, perm, n, out, dlen, is384);
 	return hipGetLastError();
 }
+template <class H>
+static void launch_hmac_var_mode(int mode, unsigned grid, hipStream_t s,
+    const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
+    const uint32_t *perm, uint64_t n, uint8_t *out, uint32_t dlen, int is384,
+    HKey<H::NW32> k, PadKW<typename H::word> pad)
+{
+	if (mode == HMAC_SIGN)
+		hmac_kernel<H, false, HMAC_SIGN><<<grid, 256, 0, s>>>(base, offsets,
+		    lens, perm, 0, 0, n, out, dlen, is384, k, pad);
+	else if (mode == HMAC_VERIFY)
+		hmac_kernel<H, false, HMAC_VERIFY><<<grid, 256, 0, s>>>(base, offsets,
+		    lens, perm, 0, 0, n, out, dlen, is384, k, pad);
+	else
+		hmac_kernel<H, false><<<grid, 256, 0, s>>>(base, offsets,
+		    lens, perm, 0, 0, n, out, dlen, is384, k, pad);
+}
+
 hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
     uint64_t stride, uint32_t fixed_len, uint64_t n, uint8_t *out,
-    uint32_t *ws, hipStream_t s)
+    uint32_t *ws, hipStream_t s, int mode)
 {
+	if (mode != HMAC_DIGESTS && offsets == nullptr)
+		return hipErrorInvalidValue;	/* datagram modes: var layout */
 	if (n == 0)
 		return hipSuccess;
 	const int halg = alg - 3;	/* HMAC row -> SHA row */
@@ -1117,6 +1169,9 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 			pad_kw256(ibits, pad);
 			hmac_kernel<Sha256H, true><<<grid, 256, 0, s>>>(base, offsets,
 			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad);
+		} else if (offsets != nullptr) {
+			launch_hmac_var_mode<Sha256H>(mode, grid, s, base, offsets,
+			    lens, perm, n, out, dlen, 0, k, pad);
 		} else {
 			hmac_kernel<Sha256H, false><<<grid, 256, 0, s>>>(base, offsets,
 			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad);
@@ -1131,6 +1186,9 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 			pad_kw512(ibits, pad);
 			hmac_kernel<Sha512, true><<<grid, 256, 0, s>>>(base, offsets,
 			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad);
+		} else if (offsets != nullptr) {
+			launch_hmac_var_mode<Sha512>(mode, grid, s, base, offsets,
+			    lens, perm, n, out, dlen, is384, k, pad);
 		} else {
 			hmac_kernel<Sha512, false><<<grid, 256, 0, s>>>(base, offsets,
 			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad);

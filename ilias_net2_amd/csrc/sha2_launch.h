@@ -39,12 +39,18 @@ hipError_t net2_bin_order(int alg, const uint32_t *lens, uint64_t n,
 /*
  * HMAC batch (alg = 4..6).  key/keylen in host memory (keylen <= block);
  * offsets == NULL selects the fixed layout (stride, fixed_len); ws as for
- * net2_launch_var (may be NULL).
+ * net2_launch_var (may be NULL).  mode (variable layout only): 0 digests to
+ * out; 1 sign datagrams in place (out = base: the first hashlen bytes of
+ * each packet receive the HMAC of the rest); 2 verify datagrams (out[i] =
+ * 0 match, 1 mismatch, 2 shorter than hashlen).
  */
+#define NET2_HMAC_MODE_DIGESTS 0
+#define NET2_HMAC_MODE_SIGN 1
+#define NET2_HMAC_MODE_VERIFY 2
 hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
     uint64_t stride, uint32_t fixed_len, uint64_t n, uint8_t *out,
-    uint32_t *ws, hipStream_t s);
+    uint32_t *ws, hipStream_t s, int mode = NET2_HMAC_MODE_DIGESTS);
 
 /* Packet-header IVs (ivlen <= 64): out = n x ivlen bytes. */
 hipError_t net2_launch_ph_iv(const uint32_t *seq, const uint32_t *flags,

@@ -624,6 +624,57 @@ NET2_EXPORT int net2_hashctx_hashiov(int alg, const void *key, size_t keylen,
 	    (uint8_t *)out);
 }
 
+/* Argument checks shared by the datagram sign / verify entry points. */
+static int check_dgram_args(int alg, const void *key, size_t keylen,
+    const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
+    uint64_t n, const void *d_ws, size_t ws_bytes)
+{
+	if (alg < NET2_HASH_HMAC_SHA256 || alg > NET2_HASH_HMAC_SHA512)
+		return EINVAL;
+	if ((size_t)kRows[alg].keylen != keylen || key == nullptr)
+		return EINVAL;
+	if (n == 0)
+		return 0;
+	if (d_base == nullptr || d_offsets == nullptr || d_lens == nullptr)
+		return EINVAL;
+	if (d_ws != nullptr && (ws_bytes < net2_sha2_dev_var_workspace(n) ||
+	    ((uintptr_t)d_ws & 3) != 0 || n > UINT32_MAX))
+		return EINVAL;
+	return check_current_device();
+}
+
+NET2_EXPORT int net2_hmac_sign_dev(int alg, const void *key, size_t keylen,
+    void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
+    uint64_t n, void *d_ws, size_t ws_bytes, void *stream)
+{
+	int rc = check_dgram_args(alg, key, keylen, d_base, d_offsets, d_lens,
+	    n, d_ws, ws_bytes);
+	if (rc != 0 || n == 0)
+		return rc;
+	HIP_TRY(net2_launch_hmac(alg, (const uint8_t *)key, keylen,
+	    (const uint8_t *)d_base, d_offsets, d_lens, 0, 0, n,
+	    (uint8_t *)d_base, (uint32_t *)d_ws, (hipStream_t)stream,
+	    NET2_HMAC_MODE_SIGN));
+	return 0;
+}
+
+NET2_EXPORT int net2_hmac_verify_dev(int alg, const void *key,
+    size_t keylen, const void *d_base, const uint64_t *d_offsets,
+    const uint32_t *d_lens, uint64_t n, uint8_t *d_result, void *d_ws,
+    size_t ws_bytes, void *stream)
+{
+	int rc = check_dgram_args(alg, key, keylen, d_base, d_offsets, d_lens,
+	    n, d_ws, ws_bytes);
+	if (rc != 0 || n == 0)
+		return rc;
+	if (d_result == nullptr)
+		return EINVAL;
+	HIP_TRY(net2_launch_hmac(alg, (const uint8_t *)key, keylen,
+	    (const uint8_t *)d_base, d_offsets, d_lens, 0, 0, n, d_result,
+	    (uint32_t *)d_ws, (hipStream_t)stream, NET2_HMAC_MODE_VERIFY));
+	return 0;
+}
+
 NET2_EXPORT int net2_hmac_dev(int alg, const void *key, size_t keylen,
     const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
     uint64_t stride, uint32_t fixed_len, uint64_t n, void *d_digests,

@@ -81,6 +81,34 @@ int net2_hmac_dev(int alg, const void *key, size_t keylen,
     uint64_t stride, uint32_t fixed_len, uint64_t n, void *d_digests,
     void *d_ws, size_t ws_bytes, void *stream);
 
+/*
+ * Batched per-datagram authenticator over datagrams laid out as hash field
+ * (hashlen bytes) || message, the wire order of types/packet.n2t: TX
+ * prepends HMAC(key, message) (net2_packet_encode, :410-427), RX removes the
+ * first hashlen bytes as the supplied hash and compares it with the HMAC of
+ * the rest (net2_packet_decode, :226-257).  Datagram i is
+ * d_base[d_offsets[i] .. + d_lens[i]); alg, key, keylen and the optional
+ * binning workspace as net2_hmac_dev.  Datagrams must not overlap.
+ * Asynchronous on stream.
+ *
+ * net2_hmac_sign_dev writes each datagram's hash field in place; datagrams
+ * shorter than hashlen are left untouched.
+ */
+int net2_hmac_sign_dev(int alg, const void *key, size_t keylen,
+    void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
+    uint64_t n, void *d_ws, size_t ws_bytes, void *stream);
+
+/*
+ * net2_hmac_verify_dev writes one byte per datagram to d_result: 0 if the
+ * hash field equals HMAC(key, message), 1 if it does not (the
+ * NET2_PDECODE_BAD of packet.n2t:254-256), 2 if the datagram is shorter
+ * than hashlen (NET2_PDECODE_BAD, :240-244).
+ */
+int net2_hmac_verify_dev(int alg, const void *key, size_t keylen,
+    const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
+    uint64_t n, uint8_t *d_result, void *d_ws, size_t ws_bytes,
+    void *stream);
+
 #ifdef __cplusplus
 }
 #endif
