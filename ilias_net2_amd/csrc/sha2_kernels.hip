@@ -35,12 +35,15 @@ namespace dev {
 /*
  * Per-kernel code-shape choices (each measured):
  *   ASM: round bodies as ordered asm blocks (NET2_ASM256, sha2_device.h);
- *   U2:  the two-block ping-pong block loop (absorb below).
+ *   U2:  the two-block ping-pong block loop (absorb below);
+ *   PAIR: the pair loop -- both 64-byte blocks of a 128-byte line requested
+ *         together, one pair ahead (absorb below).
  */
-template <bool ASM_, bool U2_>
+template <bool ASM_, bool U2_, bool PAIR_ = false>
 struct Sha256T {
 	static constexpr bool ASM = ASM_;
 	static constexpr bool U2 = U2_;
+	static constexpr bool PAIR = PAIR_;
 	typedef uint32_t word;
 	static constexpr int BLOCK = 64;	/* bytes per block */
 	static constexpr int NW32 = 16;		/* 32-bit words per block */
@@ -73,9 +76,13 @@ struct Sha256T {
 #ifndef NET2_ABSORB_U2
 #define NET2_ABSORB_U2 1
 #endif
-/* 1: the U2 block loop loads both blocks of a trip together (see absorb) */
-#ifndef NET2_PAIR_LOAD
-#define NET2_PAIR_LOAD 0
+/* pair loop (absorb): 1 for the fixed and HMAC kernels; the variable-length
+ * kernel would need 137 VGPRs (3 waves/SIMD) with it */
+#ifndef NET2_FIXED_PAIR
+#define NET2_FIXED_PAIR 1
+#endif
+#ifndef NET2_HMAC_PAIR
+#define NET2_HMAC_PAIR 1
 #endif
 #ifndef NET2_VAR_ASM
 #define NET2_VAR_ASM 0
@@ -89,13 +96,14 @@ struct Sha256T {
 #ifndef NET2_HMAC_U2
 #define NET2_HMAC_U2 1
 #endif
-typedef Sha256T<NET2_ASM256 != 0, NET2_ABSORB_U2 != 0> Sha256;	/* fixed */
+typedef Sha256T<NET2_ASM256 != 0, NET2_ABSORB_U2 != 0, NET2_FIXED_PAIR != 0> Sha256;	/* fixed */
 typedef Sha256T<NET2_VAR_ASM != 0, NET2_VAR_U2 != 0> Sha256V;	/* var */
-typedef Sha256T<NET2_HMAC_ASM != 0, NET2_HMAC_U2 != 0> Sha256H;	/* HMAC */
+typedef Sha256T<NET2_HMAC_ASM != 0, NET2_HMAC_U2 != 0, NET2_HMAC_PAIR != 0> Sha256H;	/* HMAC */
 
 struct Sha512 {
 	static constexpr bool ASM = false;
 	static constexpr bool U2 = false;	/* no prefetch: nothing to ping-pong */
+	static constexpr bool PAIR = false;	/* a 128-byte block is a whole line */
 	typedef uint64_t word;
 	static constexpr int BLOCK = 128;
 	static constexpr int NW32 = 32;
@@ -282,34 +290,58 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 	constexpr int NW32 = H::NW32;
 	const uint32_t nfull = len / H::BLOCK;
 
-	if (PREFETCH && H::U2 && NET2_PAIR_LOAD) {
+	if (PREFETCH && H::PAIR) {
 		/*
-		 * Both blocks of a trip -- one 128-byte line of an aligned packet --
-		 * requested together at the top of the trip, no prefetch: the
-		 * other waves of the SIMD cover the wait.  With a one-block-ahead
-		 * prefetch the second half of a line was requested one
-		 * compression (~20 us) after the first, long enough for many lines
-		 * to leave the 4 MB L2 of the XCD in between and be fetched again.
+		 * Pairs of blocks (one 128-byte line of an aligned packet)
+		 * requested together, one pair ahead: two pair buffers swap
+		 * roles every pair, so a trip covers four blocks.  With the
+		 * one-block-ahead prefetch below, a line's second half was
+		 * requested one compression (~20 us) after its first, long
+		 * enough for ~10 % of the lines to leave the XCD's 4 MB L2 and
+		 * be fetched again; here C2 reads exactly the payload, at the
+		 * same speed (92 VGPRs, 5 waves/SIMD;
+		 * profiles/round1/pairload_fetch.json).
 		 */
-		uint32_t k = 0;
-		for (; k + 2 <= nfull; k += 2) {
-			const uint8_t *bp = p + (size_t)k * H::BLOCK;
-			Raw<NW32> ra, rb;
-			issue_block<NW32, AMODE>(bp, ra);
-			issue_block<NW32, AMODE>(bp + H::BLOCK, rb);
-			uint32_t w[NW32];
-			finish_block<NW32, AMODE>(bp, ra, w);
-			H::compress(st, w);
-			uint32_t w2[NW32];
-			finish_block<NW32, AMODE>(bp + H::BLOCK, rb, w2);
-			H::compress(st, w2);
+		const uint32_t npairs = nfull / 2;
+		Raw<NW32> a0, a1, b0, b1;
+		if (npairs > 0) {
+			issue_block<NW32, AMODE>(p, a0);
+			issue_block<NW32, AMODE>(p + H::BLOCK, a1);
 		}
-		if (k < nfull) {
-			const uint8_t *bp = p + (size_t)k * H::BLOCK;
-			Raw<NW32> ra;
-			issue_block<NW32, AMODE>(bp, ra);
+		uint32_t q = 0;
+		for (; q + 2 <= npairs; q += 2) {
+			const uint8_t *bp = p + (size_t)q * 2 * H::BLOCK;
+			issue_block<NW32, AMODE>(bp + 2 * H::BLOCK, b0);
+			issue_block<NW32, AMODE>(bp + 3 * H::BLOCK, b1);
 			uint32_t w[NW32];
-			finish_block<NW32, AMODE>(bp, ra, w);
+			finish_block<NW32, AMODE>(bp, a0, w);
+			H::compress(st, w);
+			finish_block<NW32, AMODE>(bp + H::BLOCK, a1, w);
+			H::compress(st, w);
+			/* past the last pair: re-read pair q + 1 (in bounds, L2-hot,
+			 * unused) so a0/a1 are always defined here */
+			const uint8_t *np = bp + (q + 2 < npairs ? 4 : 2) * H::BLOCK;
+			issue_block<NW32, AMODE>(np, a0);
+			issue_block<NW32, AMODE>(np + H::BLOCK, a1);
+			finish_block<NW32, AMODE>(bp + 2 * H::BLOCK, b0, w);
+			H::compress(st, w);
+			finish_block<NW32, AMODE>(bp + 3 * H::BLOCK, b1, w);
+			H::compress(st, w);
+		}
+		if (q < npairs) {
+			const uint8_t *bp = p + (size_t)q * 2 * H::BLOCK;
+			uint32_t w[NW32];
+			finish_block<NW32, AMODE>(bp, a0, w);
+			H::compress(st, w);
+			finish_block<NW32, AMODE>(bp + H::BLOCK, a1, w);
+			H::compress(st, w);
+		}
+		if (nfull & 1) {
+			const uint8_t *bp = p + (size_t)(nfull - 1) * H::BLOCK;
+			Raw<NW32> r;
+			issue_block<NW32, AMODE>(bp, r);
+			uint32_t w[NW32];
+			finish_block<NW32, AMODE>(bp, r, w);
 			H::compress(st, w);
 		}
 	} else if (PREFETCH && H::U2) {
@@ -1113,6 +1145,14 @@ hipError_t net2_launch_var(int alg, const uint8_t *base,
 		    lens, perm, n, out, dlen, is384);
 	return hipGetLastError();
 }
+/* H without the pair loop: the VERIFY kernel measured 1.5 % faster without
+ * it (110 -> fewer VGPRs), the digest kernels 0.5-2 % faster with it
+ * (profiles/round1/hmac_pair_ab.txt). */
+template <class H> struct NoPair { typedef H type; };
+template <bool A, bool U, bool P> struct NoPair<Sha256T<A, U, P> > {
+	typedef Sha256T<A, U, false> type;
+};
+
 template <class H>
 static void launch_hmac_var_mode(int mode, unsigned grid, hipStream_t s,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
@@ -1123,8 +1163,9 @@ static void launch_hmac_var_mode(int mode, unsigned grid, hipStream_t s,
 		hmac_kernel<H, false, HMAC_SIGN><<<grid, 256, 0, s>>>(base, offsets,
 		    lens, perm, 0, 0, n, out, dlen, is384, k, pad);
 	else if (mode == HMAC_VERIFY)
-		hmac_kernel<H, false, HMAC_VERIFY><<<grid, 256, 0, s>>>(base, offsets,
-		    lens, perm, 0, 0, n, out, dlen, is384, k, pad);
+		hmac_kernel<typename NoPair<H>::type, false, HMAC_VERIFY>
+		    <<<grid, 256, 0, s>>>(base, offsets, lens, perm, 0, 0, n, out,
+		    dlen, is384, k, pad);
 	else
 		hmac_kernel<H, false><<<grid, 256, 0, s>>>(base, offsets,
 		    lens, perm, 0, 0, n, out, dlen, is384, k, pad);
