@@ -62,6 +62,12 @@ ROWS = [
 SEQS = ["SF", "SSFF", "SSSSFFFF", "SSF", "SSSF", "SSSSSSFF", "SFF", "SFFF",
         "S", "F", "SSSSSSSS" + "FFFFFFFF"]
 ROWS += [("seq " + q, "SEQ:" + q, 3) for q in SEQS]
+# Split rows: two kinds of wave on the same CU, each running a pure stream;
+# by workgroup parity the two kinds share every SIMD, by wave parity they
+# (likely) land on different SIMDs.
+ROWS += [("split by workgroup: S-only | F-only waves", "SPLITB:S|F", 3),
+         ("split by wave: S-only | F-only waves", "SPLITW:S|F", 3),
+         ("split by workgroup: SF | SF (control)", "SPLITB:SF|SF", 3)]
 
 
 def instrs(i, name, tmpl, pat):
@@ -102,6 +108,8 @@ def seq_instrs(q):
 
 
 def kernel(i, name, tmpl, pat):
+    if tmpl and tmpl.startswith("SPLIT"):
+        return split_kernel(i, tmpl)
     body = (seq_instrs(tmpl[4:]) if tmpl and tmpl.startswith("SEQ:")
             else instrs(i, name, tmpl, pat))
     n = len(body)
@@ -136,6 +144,48 @@ __global__ __launch_bounds__(256) void k{i}(uint32_t *out, uint32_t seed)
 		out[16 + blockIdx.x * 4 + threadIdx.x / 64] = (uint32_t)(t1 - t0);
 }}
 static const int kN{i} = {n * 4};	/* instructions per loop trip */
+'''
+
+
+def split_kernel(i, tmpl):
+    """Two asm loops selected per wave (uniform branch): pattern qa for
+    workgroups (SPLITB) or waves (SPLITW) of even parity, qb for odd."""
+    kind, pats = tmpl.split(":")
+    qa, qb = pats.split("|")
+    assert len(qa) == len(qb)
+    sel = "(blockIdx.x & 1)" if kind == "SPLITB" else "((threadIdx.x >> 6) & 1)"
+    clob = ", ".join(f'"v{r}"' for r in range(B, B + 48))
+    init = "".join(
+        f'"v_add_u32 v{r}, {r - B}, %1\\n\\t"\n\t    ' for r in range(B, B + 48))
+
+    def block(q):
+        loop = "".join(f'"{x}\\n\\t"\n\t    ' for x in seq_instrs(q)) * 4
+        return f'''asm volatile(
+	    {init}"s_movk_i32 s41, 0x400\\n"
+	    "1:\\n\\t"
+	    {loop}"s_sub_u32 s41, s41, 1\\n\\t"
+	    "s_cmp_lg_u32 s41, 0\\n\\t"
+	    "s_cbranch_scc1 1b\\n\\t"
+	    "v_xor_b32 %0, v8, v9\\n\\t"
+	    "v_bitop3_b32 %0, %0, v10, v11 bitop3:0x96\\n\\t"
+	    "v_bitop3_b32 %0, %0, v12, v13 bitop3:0x96\\n\\t"
+	    "v_bitop3_b32 %0, %0, v14, v15 bitop3:0x96"
+	    : "=v"(x)
+	    : "v"(v0)
+	    : {clob}, "s41", "scc");'''
+    return f'''
+__global__ __launch_bounds__(256) void k{i}(uint32_t *out, uint32_t seed)
+{{
+	uint32_t x, v0 = threadIdx.x ^ seed;
+	if (__builtin_amdgcn_readfirstlane({sel}) == 0) {{
+		{block(qa)}
+	}} else {{
+		{block(qb)}
+	}}
+	if (x == 0x12345678u)
+		out[0] = x;
+}}
+static const int kN{i} = {len(qa) * 8 * 4};	/* instructions per loop trip */
 '''
 
 
