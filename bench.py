@@ -51,6 +51,8 @@ CONFIGS = {
     # result byte per datagram
     "hmac_verify_mtu": dict(alg=4, kind="dgram_verify", n=1 << 20, length=None,
                             workload="1M x mixed {64,512,1500} B datagrams, HMAC-SHA256 verify (hash field || message), binned (8f row 1, RX)"),
+    "hmac512_verify_mtu": dict(alg=6, kind="dgram_verify", n=1 << 20, length=None,
+                               workload="1M x mixed {64,512,1500} B datagrams, HMAC-SHA512 verify (hash field || message), binned (8f row 1, RX, the negotiated default)"),
     "ph_iv": dict(alg=1, kind="ph_iv", n=1 << 20, length=16,
                   workload="1M packet headers -> 16-byte IVs, net2_ph_to_iv_dev (8f row 3)"),
 }
@@ -329,7 +331,9 @@ def main():
         ("SHA-256 IVs/s, " if cfg["kind"] == "ph_iv" else
          f"{ALG_NAMES[alg]} datagrams verified/s, " if cfg["kind"] == "dgram_verify" else
          f"{ALG_NAMES[alg]} digests/s, ") + cfg["workload"],
-        "value": round(value, 1), "unit": "digests/s", "n_gpus": ws,
+        "value": round(value, 1),
+        "unit": "datagrams/s" if cfg["kind"] == "dgram_verify" else "IVs/s" if cfg["kind"] == "ph_iv" else "digests/s",
+        "n_gpus": ws,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "prewarm_ms": args.prewarm_ms,
