@@ -132,3 +132,19 @@ def test_no_device_fails_loudly():
     with pytest.raises(_lib.Net2Error) as ei:
         h.sha256().run(b"", b"abc")
     assert ei.value.errno == errno.ENODEV
+
+
+def test_missing_library_fails_loudly():
+    """No library, no hashing: the binding raises instead of falling back
+    to any CPU path (checked in a fresh interpreter)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, NET2_SHA2_LIB="/nonexistent/libnet2_sha2.so")
+    code = ("from ilias_net2_amd import hash as h\n"
+            "try:\n"
+            "    h.sha256().run(b'', b'x')\n"
+            "except ImportError as e:\n"
+            "    print('IMPORTERROR', e)\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert "IMPORTERROR" in r.stdout and "no CPU fallback" in r.stdout, r.stdout + r.stderr
