@@ -412,20 +412,122 @@ __device__ __forceinline__ uint64_t ssig1_512(uint64_t x)
 	return xor3_64(ror64<19>(x), ror64<61>(x), shr64<6>(x));
 }
 
+/*
+ * NET2_ASM512 = 1: the bitwise half of a SHA-512 round -- the 12 rotates of
+ * Sigma1(e) and Sigma0(a) (two v_alignbit_b32 per 64-bit rotate) and the 8
+ * v_bitop3_b32 of the Sigma xors, Ch and Maj -- as one asm block with a
+ * fixed order (rotates first), as NET2_ASM256 does for SHA-256; the 64-bit
+ * sums stay in C (v_lshl_add_u64 needs register pairs, which inline asm
+ * cannot split into halves).
+ */
+#ifndef NET2_ASM512
+#define NET2_ASM512 1
+#endif
+#ifndef NET2_ASM512X	/* the schedule words too */
+#define NET2_ASM512X NET2_ASM512
+#endif
+
+__device__ __forceinline__ void bitwise512_asm(uint64_t a, uint64_t b,
+    uint64_t c, uint64_t e, uint64_t f, uint64_t g, uint64_t &S1,
+    uint64_t &CH, uint64_t &S0, uint64_t &MJ)
+{
+	uint32_t r1, r2, r3, r4, r5, r6, s1l, s1h, chl, chh, s0l, s0h, mjl, mjh;
+	/* rotr n < 32: lo = alignbit(hi, lo, n), hi = alignbit(lo, hi, n);
+	 * rotr 32 + m: lo = alignbit(lo, hi, m), hi = alignbit(hi, lo, m) */
+	asm("v_alignbit_b32 %[r1], %[eh], %[el], 14\n\t"
+	    "v_alignbit_b32 %[r2], %[eh], %[el], 18\n\t"
+	    "v_alignbit_b32 %[r3], %[el], %[eh], 9\n\t"
+	    "v_alignbit_b32 %[r4], %[el], %[eh], 14\n\t"
+	    "v_alignbit_b32 %[r5], %[el], %[eh], 18\n\t"
+	    "v_alignbit_b32 %[r6], %[eh], %[el], 9\n\t"
+	    "v_bitop3_b32 %[s1l], %[r1], %[r2], %[r3] bitop3:0x96\n\t"
+	    "v_bitop3_b32 %[s1h], %[r4], %[r5], %[r6] bitop3:0x96\n\t"
+	    "v_alignbit_b32 %[r1], %[ah], %[al], 28\n\t"
+	    "v_alignbit_b32 %[r2], %[al], %[ah], 2\n\t"
+	    "v_alignbit_b32 %[r3], %[al], %[ah], 7\n\t"
+	    "v_alignbit_b32 %[r4], %[al], %[ah], 28\n\t"
+	    "v_alignbit_b32 %[r5], %[ah], %[al], 2\n\t"
+	    "v_alignbit_b32 %[r6], %[ah], %[al], 7\n\t"
+	    "v_bitop3_b32 %[chl], %[el], %[fl], %[gl] bitop3:0xca\n\t"
+	    "v_bitop3_b32 %[chh], %[eh], %[fh], %[gh] bitop3:0xca\n\t"
+	    "v_bitop3_b32 %[s0l], %[r1], %[r2], %[r3] bitop3:0x96\n\t"
+	    "v_bitop3_b32 %[s0h], %[r4], %[r5], %[r6] bitop3:0x96\n\t"
+	    "v_bitop3_b32 %[mjl], %[al], %[bl], %[cl] bitop3:0xe8\n\t"
+	    "v_bitop3_b32 %[mjh], %[ah], %[bh], %[ch] bitop3:0xe8"
+	    : [r1] "=&v"(r1), [r2] "=&v"(r2), [r3] "=&v"(r3), [r4] "=&v"(r4),
+	      [r5] "=&v"(r5), [r6] "=&v"(r6), [s1l] "=&v"(s1l), [s1h] "=&v"(s1h),
+	      [chl] "=&v"(chl), [chh] "=&v"(chh), [s0l] "=&v"(s0l),
+	      [s0h] "=&v"(s0h), [mjl] "=&v"(mjl), [mjh] "=&v"(mjh)
+	    : [al] "v"(lo32(a)), [ah] "v"(hi32(a)), [bl] "v"(lo32(b)),
+	      [bh] "v"(hi32(b)), [cl] "v"(lo32(c)), [ch] "v"(hi32(c)),
+	      [el] "v"(lo32(e)), [eh] "v"(hi32(e)), [fl] "v"(lo32(f)),
+	      [fh] "v"(hi32(f)), [gl] "v"(lo32(g)), [gh] "v"(hi32(g)));
+	S1 = mk64(s1l, s1h);
+	CH = mk64(chl, chh);
+	S0 = mk64(s0l, s0h);
+	MJ = mk64(mjl, mjh);
+}
+
 template <int T>
 __device__ __forceinline__ void round512(uint64_t (&s)[8], uint64_t kw)
 {
 	uint64_t &a = s[(0 - T) & 7], &b = s[(1 - T) & 7], &c = s[(2 - T) & 7];
 	uint64_t &d = s[(3 - T) & 7], &e = s[(4 - T) & 7], &f = s[(5 - T) & 7];
 	uint64_t &g = s[(6 - T) & 7], &h = s[(7 - T) & 7];
+	if (NET2_ASM512) {
+		uint64_t S1, CH, S0, MJ;
+		bitwise512_asm(a, b, c, e, f, g, S1, CH, S0, MJ);
+		uint64_t t1 = h + kw + S1 + CH;
+		d += t1;
+		h = t1 + S0 + MJ;
+		return;
+	}
 	uint64_t t1 = h + kw + bsig1_512(e) + ch64(e, f, g);
 	d += t1;
 	h = t1 + bsig0_512(a) + maj64(a, b, c);
 }
 
+/*
+ * sigma0(x) and sigma1(y) of a SHA-512 schedule word with the rotates in one
+ * ordered asm block (NET2_ASM512); the 64-bit shifts (v_lshrrev_b64) are
+ * passed in, their halves read directly.
+ */
+__device__ __forceinline__ void ssigmas512_asm(uint64_t x, uint64_t y,
+    uint64_t xs, uint64_t ys, uint64_t &P0, uint64_t &P1)
+{
+	uint32_t r1, r2, r3, r4, p0l, p0h, p1l, p1h;
+	asm("v_alignbit_b32 %[r1], %[yh], %[yl], 19\n\t"
+	    "v_alignbit_b32 %[r2], %[yl], %[yh], 29\n\t"
+	    "v_alignbit_b32 %[r3], %[yl], %[yh], 19\n\t"
+	    "v_alignbit_b32 %[r4], %[yh], %[yl], 29\n\t"
+	    "v_bitop3_b32 %[p1l], %[r1], %[r2], %[ysl] bitop3:0x96\n\t"
+	    "v_bitop3_b32 %[p1h], %[r3], %[r4], %[ysh] bitop3:0x96\n\t"
+	    "v_alignbit_b32 %[r1], %[xh], %[xl], 1\n\t"
+	    "v_alignbit_b32 %[r2], %[xh], %[xl], 8\n\t"
+	    "v_alignbit_b32 %[r3], %[xl], %[xh], 1\n\t"
+	    "v_alignbit_b32 %[r4], %[xl], %[xh], 8\n\t"
+	    "v_bitop3_b32 %[p0l], %[r1], %[r2], %[xsl] bitop3:0x96\n\t"
+	    "v_bitop3_b32 %[p0h], %[r3], %[r4], %[xsh] bitop3:0x96"
+	    : [r1] "=&v"(r1), [r2] "=&v"(r2), [r3] "=&v"(r3), [r4] "=&v"(r4),
+	      [p0l] "=&v"(p0l), [p0h] "=&v"(p0h), [p1l] "=&v"(p1l),
+	      [p1h] "=&v"(p1h)
+	    : [xl] "v"(lo32(x)), [xh] "v"(hi32(x)), [yl] "v"(lo32(y)),
+	      [yh] "v"(hi32(y)), [xsl] "v"(lo32(xs)), [xsh] "v"(hi32(xs)),
+	      [ysl] "v"(lo32(ys)), [ysh] "v"(hi32(ys)));
+	P0 = mk64(p0l, p0h);
+	P1 = mk64(p1l, p1h);
+}
+
 template <int T>
 __device__ __forceinline__ uint64_t expand512(uint64_t (&w)[16])
 {
+	if (NET2_ASM512X) {
+		const uint64_t x = w[(T - 15) & 15], y = w[(T - 2) & 15];
+		uint64_t P0, P1;
+		ssigmas512_asm(x, y, shr64<7>(x), shr64<6>(y), P0, P1);
+		w[T & 15] += P1 + w[(T - 7) & 15] + P0;
+		return w[T & 15];
+	}
 	w[T & 15] += ssig1_512(w[(T - 2) & 15]) + w[(T - 7) & 15] +
 	    ssig0_512(w[(T - 15) & 15]);
 	return w[T & 15];
