@@ -4,7 +4,7 @@
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-CFGS=${PCFGS:-"c2 c4 c3 hmac"} bash tools/gpu_profile.sh
+CFGS="${PCFGS:-c2 c4 c3 hmac}" bash tools/gpu_profile.sh
 rc=$?; echo "profile rc=$rc"; [ $rc -ne 0 ] && exit $rc
 for c in ${PCFGS:-c2 c4 c3 hmac}; do
   python3 tools/pmc_summary.py --cfg $c > /dev/null || exit 1
