@@ -423,6 +423,16 @@ __device__ __forceinline__ uint64_t ssig1_512(uint64_t x)
 #ifndef NET2_ASM512
 #define NET2_ASM512 1
 #endif
+#ifndef NET2_ORD512	/* instruction order of the round's asm block */
+#define NET2_ORD512 0
+#endif
+/* orders 1 and 2 keep Sigma1's rotates live while Sigma0's are made */
+#if NET2_ORD512 == 1 || NET2_ORD512 == 2
+#define NET2_Q512_OUTS [q1] "=&v"(q1), [q2] "=&v"(q2), [q3] "=&v"(q3), \
+	[q4] "=&v"(q4), [q5] "=&v"(q5), [q6] "=&v"(q6),
+#else
+#define NET2_Q512_OUTS
+#endif
 #ifndef NET2_ASM512X	/* the schedule words too */
 #define NET2_ASM512X NET2_ASM512
 #endif
@@ -431,9 +441,77 @@ __device__ __forceinline__ void bitwise512_asm(uint64_t a, uint64_t b,
     uint64_t c, uint64_t e, uint64_t f, uint64_t g, uint64_t &S1,
     uint64_t &CH, uint64_t &S0, uint64_t &MJ)
 {
-	uint32_t r1, r2, r3, r4, r5, r6, s1l, s1h, chl, chh, s0l, s0h, mjl, mjh;
+	uint32_t r1, r2, r3, r4, r5, r6;
+#if NET2_ORD512 == 1 || NET2_ORD512 == 2
+	uint32_t q1, q2, q3, q4, q5, q6;
+#endif
+	uint32_t s1l, s1h, chl, chh, s0l, s0h, mjl, mjh;
 	/* rotr n < 32: lo = alignbit(hi, lo, n), hi = alignbit(lo, hi, n);
 	 * rotr 32 + m: lo = alignbit(lo, hi, m), hi = alignbit(hi, lo, m) */
+#if NET2_ORD512 == 1
+	asm("v_bitop3_b32 %[chl], %[el], %[fl], %[gl] bitop3:0xca\n\t"
+	    "v_bitop3_b32 %[chh], %[eh], %[fh], %[gh] bitop3:0xca\n\t"
+	    "v_bitop3_b32 %[mjl], %[al], %[bl], %[cl] bitop3:0xe8\n\t"
+	    "v_bitop3_b32 %[mjh], %[ah], %[bh], %[ch] bitop3:0xe8\n\t"
+	    "v_alignbit_b32 %[r1], %[eh], %[el], 14\n\t"
+	    "v_alignbit_b32 %[r2], %[eh], %[el], 18\n\t"
+	    "v_alignbit_b32 %[r3], %[el], %[eh], 9\n\t"
+	    "v_alignbit_b32 %[r4], %[el], %[eh], 14\n\t"
+	    "v_alignbit_b32 %[r5], %[el], %[eh], 18\n\t"
+	    "v_alignbit_b32 %[r6], %[eh], %[el], 9\n\t"
+	    "v_alignbit_b32 %[q1], %[ah], %[al], 28\n\t"
+	    "v_alignbit_b32 %[q2], %[al], %[ah], 2\n\t"
+	    "v_alignbit_b32 %[q3], %[al], %[ah], 7\n\t"
+	    "v_alignbit_b32 %[q4], %[al], %[ah], 28\n\t"
+	    "v_alignbit_b32 %[q5], %[ah], %[al], 2\n\t"
+	    "v_alignbit_b32 %[q6], %[ah], %[al], 7\n\t"
+	    "v_bitop3_b32 %[s1l], %[r1], %[r2], %[r3] bitop3:0x96\n\t"
+	    "v_bitop3_b32 %[s1h], %[r4], %[r5], %[r6] bitop3:0x96\n\t"
+	    "v_bitop3_b32 %[s0l], %[q1], %[q2], %[q3] bitop3:0x96\n\t"
+	    "v_bitop3_b32 %[s0h], %[q4], %[q5], %[q6] bitop3:0x96"
+#elif NET2_ORD512 == 2
+	asm("v_alignbit_b32 %[r1], %[eh], %[el], 14\n\t"
+	    "v_alignbit_b32 %[r2], %[eh], %[el], 18\n\t"
+	    "v_alignbit_b32 %[r3], %[el], %[eh], 9\n\t"
+	    "v_alignbit_b32 %[r4], %[el], %[eh], 14\n\t"
+	    "v_alignbit_b32 %[r5], %[el], %[eh], 18\n\t"
+	    "v_alignbit_b32 %[r6], %[eh], %[el], 9\n\t"
+	    "v_alignbit_b32 %[q1], %[ah], %[al], 28\n\t"
+	    "v_alignbit_b32 %[q2], %[al], %[ah], 2\n\t"
+	    "v_alignbit_b32 %[q3], %[al], %[ah], 7\n\t"
+	    "v_alignbit_b32 %[q4], %[al], %[ah], 28\n\t"
+	    "v_alignbit_b32 %[q5], %[ah], %[al], 2\n\t"
+	    "v_alignbit_b32 %[q6], %[ah], %[al], 7\n\t"
+	    "v_bitop3_b32 %[s1l], %[r1], %[r2], %[r3] bitop3:0x96\n\t"
+	    "v_bitop3_b32 %[s1h], %[r4], %[r5], %[r6] bitop3:0x96\n\t"
+	    "v_bitop3_b32 %[chl], %[el], %[fl], %[gl] bitop3:0xca\n\t"
+	    "v_bitop3_b32 %[chh], %[eh], %[fh], %[gh] bitop3:0xca\n\t"
+	    "v_bitop3_b32 %[s0l], %[q1], %[q2], %[q3] bitop3:0x96\n\t"
+	    "v_bitop3_b32 %[s0h], %[q4], %[q5], %[q6] bitop3:0x96\n\t"
+	    "v_bitop3_b32 %[mjl], %[al], %[bl], %[cl] bitop3:0xe8\n\t"
+	    "v_bitop3_b32 %[mjh], %[ah], %[bh], %[ch] bitop3:0xe8"
+#elif NET2_ORD512 == 3
+	asm("v_alignbit_b32 %[r1], %[eh], %[el], 14\n\t"
+	    "v_alignbit_b32 %[r2], %[eh], %[el], 18\n\t"
+	    "v_alignbit_b32 %[r3], %[el], %[eh], 9\n\t"
+	    "v_bitop3_b32 %[s1l], %[r1], %[r2], %[r3] bitop3:0x96\n\t"
+	    "v_alignbit_b32 %[r4], %[el], %[eh], 14\n\t"
+	    "v_alignbit_b32 %[r5], %[el], %[eh], 18\n\t"
+	    "v_alignbit_b32 %[r6], %[eh], %[el], 9\n\t"
+	    "v_bitop3_b32 %[s1h], %[r4], %[r5], %[r6] bitop3:0x96\n\t"
+	    "v_bitop3_b32 %[chl], %[el], %[fl], %[gl] bitop3:0xca\n\t"
+	    "v_bitop3_b32 %[chh], %[eh], %[fh], %[gh] bitop3:0xca\n\t"
+	    "v_alignbit_b32 %[r1], %[ah], %[al], 28\n\t"
+	    "v_alignbit_b32 %[r2], %[al], %[ah], 2\n\t"
+	    "v_alignbit_b32 %[r3], %[al], %[ah], 7\n\t"
+	    "v_bitop3_b32 %[s0l], %[r1], %[r2], %[r3] bitop3:0x96\n\t"
+	    "v_alignbit_b32 %[r4], %[al], %[ah], 28\n\t"
+	    "v_alignbit_b32 %[r5], %[ah], %[al], 2\n\t"
+	    "v_alignbit_b32 %[r6], %[ah], %[al], 7\n\t"
+	    "v_bitop3_b32 %[s0h], %[r4], %[r5], %[r6] bitop3:0x96\n\t"
+	    "v_bitop3_b32 %[mjl], %[al], %[bl], %[cl] bitop3:0xe8\n\t"
+	    "v_bitop3_b32 %[mjh], %[ah], %[bh], %[ch] bitop3:0xe8"
+#else
 	asm("v_alignbit_b32 %[r1], %[eh], %[el], 14\n\t"
 	    "v_alignbit_b32 %[r2], %[eh], %[el], 18\n\t"
 	    "v_alignbit_b32 %[r3], %[el], %[eh], 9\n\t"
@@ -454,8 +532,10 @@ __device__ __forceinline__ void bitwise512_asm(uint64_t a, uint64_t b,
 	    "v_bitop3_b32 %[s0h], %[r4], %[r5], %[r6] bitop3:0x96\n\t"
 	    "v_bitop3_b32 %[mjl], %[al], %[bl], %[cl] bitop3:0xe8\n\t"
 	    "v_bitop3_b32 %[mjh], %[ah], %[bh], %[ch] bitop3:0xe8"
+#endif
 	    : [r1] "=&v"(r1), [r2] "=&v"(r2), [r3] "=&v"(r3), [r4] "=&v"(r4),
-	      [r5] "=&v"(r5), [r6] "=&v"(r6), [s1l] "=&v"(s1l), [s1h] "=&v"(s1h),
+	      [r5] "=&v"(r5), [r6] "=&v"(r6), NET2_Q512_OUTS
+	      [s1l] "=&v"(s1l), [s1h] "=&v"(s1h),
 	      [chl] "=&v"(chl), [chh] "=&v"(chh), [s0l] "=&v"(s0l),
 	      [s0h] "=&v"(s0h), [mjl] "=&v"(mjl), [mjh] "=&v"(mjh)
 	    : [al] "v"(lo32(a)), [ah] "v"(hi32(a)), [bl] "v"(lo32(b)),
