@@ -90,6 +90,15 @@ struct Sha256T {
 #ifndef NET2_VAR_U2
 #define NET2_VAR_U2 1
 #endif
+/* prefetch in the byte-aligned (A1) path of the variable-length and HMAC
+ * kernels: every path of a kernel shares its VGPR allocation, and the A1
+ * path's double buffer (17 words each) sets it */
+#ifndef NET2_VAR_A1_PREFETCH
+#define NET2_VAR_A1_PREFETCH 1
+#endif
+#ifndef NET2_HMAC_A1_PREFETCH
+#define NET2_HMAC_A1_PREFETCH 1
+#endif
 #ifndef NET2_HMAC_ASM
 #define NET2_HMAC_ASM 1
 #endif
@@ -518,7 +527,8 @@ __global__ __launch_bounds__(256) void var_kernel(const uint8_t *__restrict__ ba
 	else if (__all((reinterpret_cast<uintptr_t>(p) & 3) == 0))
 		digest_one<H, AMODE_A4, false>(p, len, is384, nullptr, st);
 	else
-		digest_one<H, AMODE_A1, false>(p, len, is384, nullptr, st);
+		digest_one<H, AMODE_A1, false, NET2_VAR_A1_PREFETCH != 0>(p, len,
+		    is384, nullptr, st);
 	materialize<H>(st);
 	if (!live)
 		return;
@@ -587,13 +597,13 @@ __device__ __forceinline__ void load_mid(const uint32_t (*mid)[16], int which,
 }
 
 /* Inner hash from the ipad midstate, one address mode. */
-template <class H, int AMODE, bool PADCONST>
+template <class H, int AMODE, bool PADCONST, bool PREFETCH = H::PREFETCH>
 __device__ __forceinline__ void hmac_inner(const uint8_t *p, uint32_t len,
     const uint32_t (*mid)[16], const typename H::word *kw,
     typename H::State &st)
 {
 	load_mid<H>(mid, 0, st);
-	absorb<H, AMODE>(p, len, st);
+	absorb<H, AMODE, PREFETCH>(p, len, st);
 	finish<H, PADCONST>(p, len, ((uint64_t)len + H::BLOCK) << 3, kw, st);
 }
 
@@ -610,7 +620,8 @@ __device__ __forceinline__ void hmac_lane(const uint8_t *p, uint32_t len,
 	else if (amode == AMODE_A4)
 		hmac_inner<H, AMODE_A4, PADCONST>(p, len, mid, kw, st);
 	else
-		hmac_inner<H, AMODE_A1, PADCONST>(p, len, mid, kw, st);
+		hmac_inner<H, AMODE_A1, PADCONST, NET2_HMAC_A1_PREFETCH != 0>(p,
+		    len, mid, kw, st);
 
 	/* outer: one block = inner digest || 0x80 || 0... || bit count */
 	uint32_t w[NW32];
