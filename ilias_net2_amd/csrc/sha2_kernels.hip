@@ -527,8 +527,9 @@ __global__ __launch_bounds__(256) void var_kernel(const uint8_t *__restrict__ ba
 	else if (__all((reinterpret_cast<uintptr_t>(p) & 3) == 0))
 		digest_one<H, AMODE_A4, false>(p, len, is384, nullptr, st);
 	else
-		digest_one<H, AMODE_A1, false, NET2_VAR_A1_PREFETCH != 0>(p, len,
-		    is384, nullptr, st);
+		digest_one<H, AMODE_A1, false,
+		    H::PREFETCH && NET2_VAR_A1_PREFETCH != 0>(p, len, is384,
+		    nullptr, st);
 	materialize<H>(st);
 	if (!live)
 		return;
@@ -620,8 +621,8 @@ __device__ __forceinline__ void hmac_lane(const uint8_t *p, uint32_t len,
 	else if (amode == AMODE_A4)
 		hmac_inner<H, AMODE_A4, PADCONST>(p, len, mid, kw, st);
 	else
-		hmac_inner<H, AMODE_A1, PADCONST, NET2_HMAC_A1_PREFETCH != 0>(p,
-		    len, mid, kw, st);
+		hmac_inner<H, AMODE_A1, PADCONST,
+		    H::PREFETCH && NET2_HMAC_A1_PREFETCH != 0>(p, len, mid, kw, st);
 
 	/* outer: one block = inner digest || 0x80 || 0... || bit count */
 	uint32_t w[NW32];
