@@ -76,8 +76,10 @@ struct Sha256T {
 #ifndef NET2_ABSORB_U2
 #define NET2_ABSORB_U2 1
 #endif
-/* pair loop (absorb): 1 for the fixed and HMAC kernels; the variable-length
- * kernel would need 137 VGPRs (3 waves/SIMD) with it */
+/* pair loop (absorb) per kernel: fixed, HMAC digests and the variable-length
+ * kernel (137 VGPRs, 3 waves/SIMD, still +0.7 % on C3:
+ * profiles/round1/var_pair_ab.txt); the RX verify kernel keeps the one-block
+ * loop (NoPair below) */
 #ifndef NET2_FIXED_PAIR
 #define NET2_FIXED_PAIR 1
 #endif
@@ -106,7 +108,10 @@ struct Sha256T {
 #define NET2_HMAC_U2 1
 #endif
 typedef Sha256T<NET2_ASM256 != 0, NET2_ABSORB_U2 != 0, NET2_FIXED_PAIR != 0> Sha256;	/* fixed */
-typedef Sha256T<NET2_VAR_ASM != 0, NET2_VAR_U2 != 0> Sha256V;	/* var */
+#ifndef NET2_VAR_PAIR
+#define NET2_VAR_PAIR 1
+#endif
+typedef Sha256T<NET2_VAR_ASM != 0, NET2_VAR_U2 != 0, NET2_VAR_PAIR != 0> Sha256V;	/* var */
 typedef Sha256T<NET2_HMAC_ASM != 0, NET2_HMAC_U2 != 0, NET2_HMAC_PAIR != 0> Sha256H;	/* HMAC */
 
 struct Sha512 {
