@@ -18,6 +18,9 @@
 #include <stdint.h>
 #include <string.h>
 #include <sys/uio.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <time.h>
 
 #include <algorithm>
 #include <atomic>
@@ -169,9 +172,13 @@ struct Slot {
 		}
 		if (in <= cap_in && n <= cap_n)
 			return 0;
+		/* grow both dimensions monotonically, with headroom: chunks of a
+		 * variable-length batch differ slightly in bytes and packet count,
+		 * and re-sizing to each one exactly re-allocated the pinned
+		 * buffers (~10 ms) on every other chunk */
+		in = std::max<size_t>({in + in / 8, cap_in, 4096});
+		n = std::max<size_t>({n + n / 4, cap_n, 64});
 		release();
-		in = std::max<size_t>(in, 4096);
-		n = std::max<size_t>(n, 64);
 		HIP_TRY(hipHostMalloc((void **)&h_in, in, hipHostMallocDefault));
 		HIP_TRY(hipHostMalloc((void **)&h_dig, n * 64,
 		    hipHostMallocDefault));
@@ -244,6 +251,42 @@ void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes)
 		x.join();
 }
 
+/* NET2_SHA2_DEBUG_TIMING=1: per-chunk host timings on stderr. */
+bool dbg_timing()
+{
+	static const bool on = getenv("NET2_SHA2_DEBUG_TIMING") != nullptr;
+	return on;
+}
+double dbg_now()
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
+/* Gather n packets into the staging buffer at dst_off[], split over a few
+ * threads when the chunk is large (the single-thread gather of MTU-sized
+ * datagrams ran well below the PCIe rate). */
+void par_gather(uint8_t *dst, const uint64_t *dst_off, const uint8_t *base,
+    const uint64_t *offsets, const uint32_t *lens, uint64_t n, size_t bytes)
+{
+	auto run = [=](uint64_t a, uint64_t b) {
+		for (uint64_t i = a; i < b; i++)
+			memcpy(dst + dst_off[i], base + offsets[i], lens[i]);
+	};
+	const size_t nt = std::min<size_t>(8, std::max<size_t>(1, bytes >> 23));
+	if (nt <= 1 || n < 2 * nt) {
+		run(0, n);
+		return;
+	}
+	std::vector<std::thread> th;
+	for (size_t t = 1; t < nt; t++)
+		th.emplace_back(run, n * t / nt, n * (t + 1) / nt);
+	run(0, n / nt);
+	for (std::thread &x : th)
+		x.join();
+}
+
 /*
  * One chunk [lo, hi) of the caller's packets into slot s: H2D (straight from
  * the caller's buffer when it is pinned and the layout is fixed, else
@@ -268,8 +311,11 @@ int enqueue_chunk(Slot &s, int alg, const uint8_t *base,
 		for (uint64_t i = lo; i < hi; i++)
 			bytes += ((size_t)lens[i] + 15) & ~(size_t)15;
 	}
+	const double tr0 = dbg_now();
 	if ((rc = s.reserve(bytes, n)) != 0)
 		return rc;
+	if (dbg_timing())
+		fprintf(stderr, "net2: reserve %.3f ms\n", dbg_now() - tr0);
 
 	if (offsets == nullptr && src_pinned) {
 		HIP_TRY(hipMemcpyAsync(s.d_in, base + lo * stride, bytes,
@@ -296,18 +342,22 @@ int enqueue_chunk(Slot &s, int alg, const uint8_t *base,
 		size_t at = 0;
 		for (uint64_t i = 0; i < n; i++) {
 			const uint32_t l = lens[lo + i];
-			memcpy(s.h_in + at, base + offsets[lo + i], l);
 			s.h_off[i] = at;
 			s.h_len[i] = l;
 			at += ((size_t)l + 15) & ~(size_t)15;
 		}
+		const double tg0 = dbg_now();
+		par_gather(s.h_in, s.h_off, base, offsets + lo, lens + lo, n, bytes);
+		if (dbg_timing())
+			fprintf(stderr, "net2: gather %zu B, %llu packets: %.3f ms\n",
+			    bytes, (unsigned long long)n, dbg_now() - tg0);
 		HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
 		    hipMemcpyHostToDevice, s.stream));
 		HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, n * 8,
 		    hipMemcpyHostToDevice, s.stream));
 		HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, n * 4,
 		    hipMemcpyHostToDevice, s.stream));
-		HIP_TRY(net2_launch_var(alg, s.d_in, s.d_off, s.d_len, n,
+			HIP_TRY(net2_launch_var(alg, s.d_in, s.d_off, s.d_len, n,
 		    s.d_dig, n >= 4096 ? s.d_ws : nullptr, s.stream));
 	}
 	HIP_TRY(hipMemcpyAsync(dst_pinned ? user_dig : s.h_dig, s.d_dig,
@@ -345,6 +395,7 @@ int run_device_slice(size_t didx, int alg, const uint8_t *base,
 	const bool dst_pinned = is_pinned(digests);
 	for (uint64_t at = lo; at < hi && rc == 0;) {
 		/* chunk end: at most kChunkBytes of (padded) payload */
+		const double tc0 = dbg_now();
 		uint64_t end = at;
 		size_t bytes = 0;
 		if (offsets == nullptr) {
@@ -360,11 +411,18 @@ int run_device_slice(size_t didx, int alg, const uint8_t *base,
 			}
 		}
 		Slot &s = c->slot[cur];
+		const double td0 = dbg_now();
 		if ((rc = drain(s)) != 0)
 			break;
+		if (dbg_timing())
+			fprintf(stderr, "net2: drain wait %.3f ms\n", dbg_now() - td0);
+		const double te0 = dbg_now();
 		rc = enqueue_chunk(s, alg, base, offsets, lens, stride,
 		    fixed_len, at, end, digests + at * dl, src_pinned,
 		    dst_pinned);
+		if (dbg_timing())
+			fprintf(stderr, "net2: enqueue %.3f ms (chunk-end scan %.3f ms)\n",
+			    dbg_now() - te0, te0 - tc0);
 		at = end;
 		cur ^= 1;
 	}
