@@ -236,6 +236,20 @@ def test_host_batch(dev, batch, oracle_mod):
     assert np.array_equal(got, want)
 
 
+def test_host_batch_var_multichunk(dev, batch, oracle_mod):
+    """Variable layout from pageable memory over several 64 MiB chunks whose
+    byte and packet counts differ (staging growth, parallel gather), twice
+    so the second call reuses the grown staging buffers."""
+    lens = synth.mixed_lengths(26, 200000, choices=(64, 512, 1500, 1472, 20, 9000))
+    data, offs = synth.packed(27, lens, align=4, gap=3)
+    want = oracle_mod.batch(1, data, offsets=offs, lens=lens,
+                            nthreads=CPU_THREADS)
+    for _ in range(2):
+        got = batch.digest_host(1, data, offsets=offs, lens=lens, max_devices=1)
+        bad = np.nonzero((got != want).any(axis=1))[0]
+        assert bad.size == 0, bad[:8]
+
+
 # ---- BASELINE.json configs at full size ------------------------------------
 
 def _full_fixed(dev, batch, oracle_mod, alg, seed):
