@@ -264,25 +264,56 @@ double dbg_now()
 	return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
 }
 
-/* Gather n packets into the staging buffer at dst_off[], split over a few
- * threads when the chunk is large (the single-thread gather of MTU-sized
- * datagrams ran well below the PCIe rate). */
-void par_gather(uint8_t *dst, const uint64_t *dst_off, const uint8_t *base,
-    const uint64_t *offsets, const uint32_t *lens, uint64_t n, size_t bytes)
+/*
+ * Pack n packets into the staging buffer with 16-byte aligned starts, and
+ * write their staged offsets and lengths, split over a few threads when the
+ * chunk is large: each thread sums its range's padded lengths, the ranges'
+ * starts are a prefix over threads, then each thread writes its offsets and
+ * copies its packets (a serial prefix and gather over MTU-sized datagrams
+ * held the host path well below the PCIe rate).  Up to 16 threads, the
+ * CPU share of one GPU on an MI355X node.
+ */
+#ifndef NET2_PACK_THREADS
+#define NET2_PACK_THREADS 16
+#endif
+constexpr size_t kPackThreads = NET2_PACK_THREADS;
+
+void par_pack(uint8_t *dst, uint64_t *dst_off, uint32_t *dst_len,
+    const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
+    uint64_t n, size_t bytes)
 {
-	auto run = [=](uint64_t a, uint64_t b) {
-		for (uint64_t i = a; i < b; i++)
-			memcpy(dst + dst_off[i], base + offsets[i], lens[i]);
+	const size_t nt = std::min<size_t>(kPackThreads,
+	    std::max<size_t>(1, bytes >> 22));
+	auto fill = [=](uint64_t a, uint64_t b, size_t at) {
+		for (uint64_t i = a; i < b; i++) {
+			const uint32_t l = lens[i];
+			dst_off[i] = at;
+			dst_len[i] = l;
+			memcpy(dst + at, base + offsets[i], l);
+			at += ((size_t)l + 15) & ~(size_t)15;
+		}
 	};
-	const size_t nt = std::min<size_t>(8, std::max<size_t>(1, bytes >> 23));
 	if (nt <= 1 || n < 2 * nt) {
-		run(0, n);
+		fill(0, n, 0);
 		return;
 	}
+	std::vector<size_t> start(nt + 1, 0);
 	std::vector<std::thread> th;
+	for (size_t t = 0; t < nt; t++)
+		th.emplace_back([&, t]() {
+			size_t sum = 0;
+			for (uint64_t i = n * t / nt; i < n * (t + 1) / nt; i++)
+				sum += ((size_t)lens[i] + 15) & ~(size_t)15;
+			start[t + 1] = sum;
+		});
+	for (std::thread &x : th)
+		x.join();
+	th.clear();
+	for (size_t t = 1; t <= nt; t++)
+		start[t] += start[t - 1];
 	for (size_t t = 1; t < nt; t++)
-		th.emplace_back(run, n * t / nt, n * (t + 1) / nt);
-	run(0, n / nt);
+		th.emplace_back(fill, n * t / nt, n * (t + 1) / nt, start[t]);
+	fill(0, n / nt, 0);
 	for (std::thread &x : th)
 		x.join();
 }
@@ -296,21 +327,19 @@ void par_gather(uint8_t *dst, const uint64_t *dst_off, const uint8_t *base,
  */
 int enqueue_chunk(Slot &s, int alg, const uint8_t *base,
     const uint64_t *offsets, const uint32_t *lens, uint64_t stride,
-    uint32_t fixed_len, uint64_t lo, uint64_t hi, uint8_t *user_dig,
-    bool src_pinned, bool dst_pinned)
+    uint32_t fixed_len, uint64_t lo, uint64_t hi, size_t var_bytes,
+    uint8_t *user_dig, bool src_pinned, bool dst_pinned)
 {
 	const uint64_t n = hi - lo;
 	const int dl = digest_len(alg);
-	size_t bytes = 0;
+	size_t bytes;
 	int rc;
 
-	if (offsets == nullptr) {
+	if (offsets == nullptr)
 		bytes = src_pinned ? (size_t)(n - 1) * stride + fixed_len
 		    : (size_t)n * ((fixed_len + 15) & ~15u);
-	} else {
-		for (uint64_t i = lo; i < hi; i++)
-			bytes += ((size_t)lens[i] + 15) & ~(size_t)15;
-	}
+	else
+		bytes = var_bytes;	/* padded total, from the chunk scan */
 	const double tr0 = dbg_now();
 	if ((rc = s.reserve(bytes, n)) != 0)
 		return rc;
@@ -339,17 +368,11 @@ int enqueue_chunk(Slot &s, int alg, const uint8_t *base,
 		HIP_TRY(net2_launch_fixed(alg, s.d_in, st, fixed_len, n,
 		    s.d_dig, s.stream));
 	} else {
-		size_t at = 0;
-		for (uint64_t i = 0; i < n; i++) {
-			const uint32_t l = lens[lo + i];
-			s.h_off[i] = at;
-			s.h_len[i] = l;
-			at += ((size_t)l + 15) & ~(size_t)15;
-		}
 		const double tg0 = dbg_now();
-		par_gather(s.h_in, s.h_off, base, offsets + lo, lens + lo, n, bytes);
+		par_pack(s.h_in, s.h_off, s.h_len, base, offsets + lo, lens + lo,
+		    n, bytes);
 		if (dbg_timing())
-			fprintf(stderr, "net2: gather %zu B, %llu packets: %.3f ms\n",
+			fprintf(stderr, "net2: pack %zu B, %llu packets: %.3f ms\n",
 			    bytes, (unsigned long long)n, dbg_now() - tg0);
 		HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
 		    hipMemcpyHostToDevice, s.stream));
@@ -418,7 +441,7 @@ int run_device_slice(size_t didx, int alg, const uint8_t *base,
 			fprintf(stderr, "net2: drain wait %.3f ms\n", dbg_now() - td0);
 		const double te0 = dbg_now();
 		rc = enqueue_chunk(s, alg, base, offsets, lens, stride,
-		    fixed_len, at, end, digests + at * dl, src_pinned,
+		    fixed_len, at, end, bytes, digests + at * dl, src_pinned,
 		    dst_pinned);
 		if (dbg_timing())
 			fprintf(stderr, "net2: enqueue %.3f ms (chunk-end scan %.3f ms)\n",
