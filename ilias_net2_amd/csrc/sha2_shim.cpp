@@ -24,6 +24,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -198,7 +200,102 @@ struct Slot {
 	}
 };
 
+/*
+ * Host worker threads for packing staged chunks, kept alive between chunks
+ * and calls: spawning and joining 16 threads twice per 64 MiB chunk cost
+ * about a third of the pack itself.  run(nt, f) calls f(0) on the caller and
+ * f(1..nt-1) on workers and returns when all are done.  Workers spin for
+ * about half a millisecond after a job (the next chunk's job usually comes
+ * sooner), then sleep on a condition variable.  The job word packs the
+ * generation with nt, so a worker that wakes late never runs a job it is
+ * not counted in.  Pools are never destroyed (their threads are detached
+ * and may be parked at process exit).
+ */
+#ifndef NET2_POOL_SPIN_US
+#define NET2_POOL_SPIN_US 500
+#endif
+
+class WorkPool {
+public:
+	template <class F>
+	void run(size_t nt, const F &f)
+	{
+		if (nt <= 1) {
+			f((size_t)0);
+			return;
+		}
+		grow(nt - 1);
+		const std::function<void(size_t)> job = f;
+		job_ = &job;
+		pending_.store(nt - 1, std::memory_order_relaxed);
+		{
+			std::lock_guard<std::mutex> g(m_);
+			word_.store(((word_.load(std::memory_order_relaxed) >> 8) + 1)
+			    << 8 | nt, std::memory_order_release);
+		}
+		cv_.notify_all();
+		f((size_t)0);
+		while (pending_.load(std::memory_order_acquire) != 0)
+			__builtin_ia32_pause();
+	}
+
+private:
+	void grow(size_t want)
+	{
+		/* a new worker starts from the word before this job's bump */
+		const uint64_t now = word_.load(std::memory_order_relaxed);
+		while (nworkers_ < want) {
+			const size_t idx = ++nworkers_;
+			std::thread([this, idx, now]() { worker(idx, now); })
+			    .detach();
+		}
+	}
+
+	void worker(size_t idx, uint64_t seen)
+	{
+		for (;;) {
+			uint64_t w = seen;
+			const double t0 = dbg_clock();
+			for (unsigned i = 1; w == seen; i++) {
+				__builtin_ia32_pause();
+				w = word_.load(std::memory_order_acquire);
+				if ((i & 1023) == 0 &&
+				    dbg_clock() - t0 > NET2_POOL_SPIN_US * 1e-3)
+					break;
+			}
+			if (w == seen) {
+				std::unique_lock<std::mutex> lk(m_);
+				cv_.wait(lk, [&]() {
+					return word_.load(std::memory_order_acquire)
+					    != seen;
+				});
+				w = word_.load(std::memory_order_acquire);
+			}
+			seen = w;
+			if (idx < (w & 0xff)) {
+				(*job_)(idx);
+				pending_.fetch_sub(1, std::memory_order_release);
+			}
+		}
+	}
+
+	static double dbg_clock()
+	{
+		struct timespec ts;
+		clock_gettime(CLOCK_MONOTONIC, &ts);
+		return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+	}
+
+	std::atomic<uint64_t> word_{0};	/* generation << 8 | nt */
+	std::atomic<size_t> pending_{0};
+	const std::function<void(size_t)> *job_ = nullptr;
+	size_t nworkers_ = 0;
+	std::mutex m_;
+	std::condition_variable cv_;
+};
+
 struct DeviceCtx {
+	WorkPool *pool = new WorkPool();	/* never freed, see WorkPool */
 	std::mutex mu;		/* one host-memory batch per device at a time */
 	Slot slot[2];
 	Slot small;		/* single-message path (hashiov, HMAC keys) */
@@ -232,23 +329,16 @@ bool is_pinned(const void *p)
 	return a.type == hipMemoryTypeHost;
 }
 
-/* memcpy of a large range split over a few threads (staging copies). */
-void par_memcpy(uint8_t *dst, const uint8_t *src, size_t bytes)
+/* memcpy of a large range split over the pool's threads (staging copies). */
+void par_memcpy(WorkPool &pool, uint8_t *dst, const uint8_t *src,
+    size_t bytes)
 {
 	const size_t piece = 8u << 20;
 	const size_t nt = std::min<size_t>(8, (bytes + piece - 1) / piece);
-	if (nt <= 1) {
-		memcpy(dst, src, bytes);
-		return;
-	}
-	std::vector<std::thread> th;
-	for (size_t t = 1; t < nt; t++) {
-		size_t a = bytes * t / nt, b = bytes * (t + 1) / nt;
-		th.emplace_back([=]() { memcpy(dst + a, src + a, b - a); });
-	}
-	memcpy(dst, src, bytes / nt);
-	for (std::thread &x : th)
-		x.join();
+	pool.run(nt, [=](size_t t) {
+		const size_t a = bytes * t / nt, b = bytes * (t + 1) / nt;
+		memcpy(dst + a, src + a, b - a);
+	});
 }
 
 /* NET2_SHA2_DEBUG_TIMING=1: per-chunk host timings on stderr. */
@@ -265,57 +355,58 @@ double dbg_now()
 }
 
 /*
- * Pack n packets into the staging buffer with 16-byte aligned starts, and
- * write their staged offsets and lengths, split over a few threads when the
- * chunk is large: each thread sums its range's padded lengths, the ranges'
- * starts are a prefix over threads, then each thread writes its offsets and
- * copies its packets (a serial prefix and gather over MTU-sized datagrams
- * held the host path well below the PCIe rate).  Up to 16 threads, the
- * CPU share of one GPU on an MI355X node.
+ * Pack n packets into pinned staging with 16-byte aligned starts and write
+ * their staged offsets and lengths, split over up to kPackThreads threads
+ * (the CPU share of one GPU on an MI355X node): pack_sizes sums each
+ * thread's range of padded lengths (the chunk's byte count, and each
+ * range's start), pack_fill then writes offsets and copies packets.  A
+ * serial scan and gather over MTU-sized datagrams held the host path well
+ * below the PCIe rate.
  */
 #ifndef NET2_PACK_THREADS
 #define NET2_PACK_THREADS 16
 #endif
 constexpr size_t kPackThreads = NET2_PACK_THREADS;
 
-void par_pack(uint8_t *dst, uint64_t *dst_off, uint32_t *dst_len,
-    const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
-    uint64_t n, size_t bytes)
+struct PackPlan {
+	size_t nt = 1;
+	size_t start[kPackThreads + 1] = {};	/* start[nt] = total bytes */
+};
+
+PackPlan pack_sizes(WorkPool &pool, const uint32_t *lens, uint64_t n)
 {
-	const size_t nt = std::min<size_t>(kPackThreads,
-	    std::max<size_t>(1, bytes >> 22));
-	auto fill = [=](uint64_t a, uint64_t b, size_t at) {
-		for (uint64_t i = a; i < b; i++) {
+	PackPlan pl;
+	/* one thread per ~4k packets (the fill copies ~MiBs each) */
+	pl.nt = std::min<size_t>(kPackThreads, std::max<size_t>(1, n >> 12));
+	size_t *st = pl.start;
+	const size_t nt = pl.nt;
+	pool.run(nt, [=](size_t t) {
+		size_t sum = 0;
+		for (uint64_t i = n * t / nt; i < n * (t + 1) / nt; i++)
+			sum += ((size_t)lens[i] + 15) & ~(size_t)15;
+		st[t + 1] = sum;
+	});
+	for (size_t t = 1; t <= nt; t++)
+		st[t] += st[t - 1];
+	return pl;
+}
+
+void pack_fill(WorkPool &pool, const PackPlan &pl, uint8_t *dst, uint64_t *dst_off,
+    uint32_t *dst_len, const uint8_t *base, const uint64_t *offsets,
+    const uint32_t *lens, uint64_t n)
+{
+	const size_t nt = pl.nt;
+	const size_t *st = pl.start;
+	pool.run(nt, [=](size_t t) {
+		size_t at = st[t];
+		for (uint64_t i = n * t / nt; i < n * (t + 1) / nt; i++) {
 			const uint32_t l = lens[i];
 			dst_off[i] = at;
 			dst_len[i] = l;
 			memcpy(dst + at, base + offsets[i], l);
 			at += ((size_t)l + 15) & ~(size_t)15;
 		}
-	};
-	if (nt <= 1 || n < 2 * nt) {
-		fill(0, n, 0);
-		return;
-	}
-	std::vector<size_t> start(nt + 1, 0);
-	std::vector<std::thread> th;
-	for (size_t t = 0; t < nt; t++)
-		th.emplace_back([&, t]() {
-			size_t sum = 0;
-			for (uint64_t i = n * t / nt; i < n * (t + 1) / nt; i++)
-				sum += ((size_t)lens[i] + 15) & ~(size_t)15;
-			start[t + 1] = sum;
-		});
-	for (std::thread &x : th)
-		x.join();
-	th.clear();
-	for (size_t t = 1; t <= nt; t++)
-		start[t] += start[t - 1];
-	for (size_t t = 1; t < nt; t++)
-		th.emplace_back(fill, n * t / nt, n * (t + 1) / nt, start[t]);
-	fill(0, n / nt, 0);
-	for (std::thread &x : th)
-		x.join();
+	});
 }
 
 /*
@@ -325,21 +416,24 @@ void par_pack(uint8_t *dst, uint64_t *dst_off, uint32_t *dst_len,
  * starts), kernel, D2H of the digests (straight into the caller's buffer
  * when that is pinned).
  */
-int enqueue_chunk(Slot &s, int alg, const uint8_t *base,
+int enqueue_chunk(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
     const uint64_t *offsets, const uint32_t *lens, uint64_t stride,
-    uint32_t fixed_len, uint64_t lo, uint64_t hi, size_t var_bytes,
-    uint8_t *user_dig, bool src_pinned, bool dst_pinned)
+    uint32_t fixed_len, uint64_t lo, uint64_t hi, uint8_t *user_dig,
+    bool src_pinned, bool dst_pinned)
 {
 	const uint64_t n = hi - lo;
 	const int dl = digest_len(alg);
 	size_t bytes;
 	int rc;
+	PackPlan plan;
 
-	if (offsets == nullptr)
+	if (offsets == nullptr) {
 		bytes = src_pinned ? (size_t)(n - 1) * stride + fixed_len
 		    : (size_t)n * ((fixed_len + 15) & ~15u);
-	else
-		bytes = var_bytes;	/* padded total, from the chunk scan */
+	} else {
+		plan = pack_sizes(pool, lens + lo, n);
+		bytes = plan.start[plan.nt];
+	}
 	const double tr0 = dbg_now();
 	if ((rc = s.reserve(bytes, n)) != 0)
 		return rc;
@@ -356,12 +450,18 @@ int enqueue_chunk(Slot &s, int alg, const uint8_t *base,
 		if (st == stride) {
 			/* contiguous; the caller's buffer ends at the last
 			 * packet's last byte, not at a stride boundary */
-			par_memcpy(s.h_in, base + lo * stride,
+			par_memcpy(pool, s.h_in, base + lo * stride,
 			    (size_t)(n - 1) * stride + fixed_len);
 		} else {
-			for (uint64_t i = 0; i < n; i++)
-				memcpy(s.h_in + i * st, base + (lo + i) * stride,
-				    fixed_len);
+			const size_t nt = std::min<size_t>(kPackThreads,
+			    std::max<size_t>(1, bytes >> 22));
+			uint8_t *dst = s.h_in;
+			const uint8_t *src = base + lo * stride;
+			pool.run(nt, [=](size_t t) {
+				for (uint64_t i = n * t / nt; i < n * (t + 1) / nt; i++)
+					memcpy(dst + i * st, src + i * stride,
+					    fixed_len);
+			});
 		}
 		HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
 		    hipMemcpyHostToDevice, s.stream));
@@ -369,8 +469,8 @@ int enqueue_chunk(Slot &s, int alg, const uint8_t *base,
 		    s.d_dig, s.stream));
 	} else {
 		const double tg0 = dbg_now();
-		par_pack(s.h_in, s.h_off, s.h_len, base, offsets + lo, lens + lo,
-		    n, bytes);
+		pack_fill(pool, plan, s.h_in, s.h_off, s.h_len, base, offsets + lo,
+		    lens + lo, n);
 		if (dbg_timing())
 			fprintf(stderr, "net2: pack %zu B, %llu packets: %.3f ms\n",
 			    bytes, (unsigned long long)n, dbg_now() - tg0);
@@ -380,7 +480,7 @@ int enqueue_chunk(Slot &s, int alg, const uint8_t *base,
 		    hipMemcpyHostToDevice, s.stream));
 		HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, n * 4,
 		    hipMemcpyHostToDevice, s.stream));
-			HIP_TRY(net2_launch_var(alg, s.d_in, s.d_off, s.d_len, n,
+		HIP_TRY(net2_launch_var(alg, s.d_in, s.d_off, s.d_len, n,
 		    s.d_dig, n >= 4096 ? s.d_ws : nullptr, s.stream));
 	}
 	HIP_TRY(hipMemcpyAsync(dst_pinned ? user_dig : s.h_dig, s.d_dig,
@@ -416,23 +516,24 @@ int run_device_slice(size_t didx, int alg, const uint8_t *base,
 	HIP_TRY(hipSetDevice(devices()[didx]));
 	const bool src_pinned = offsets == nullptr && is_pinned(base);
 	const bool dst_pinned = is_pinned(digests);
+	/*
+	 * Packets per chunk: kChunkBytes of (padded) payload at the slice's
+	 * mean packet size.  A chunk of unusually large packets just grows the
+	 * staging (Slot::reserve); the exact byte count comes from pack_sizes.
+	 */
+	uint64_t per_chunk;
+	if (offsets == nullptr) {
+		const size_t per = std::max<size_t>((fixed_len + 15) & ~15u, 16);
+		per_chunk = std::max<size_t>(kChunkBytes / per, 1);
+	} else {
+		const PackPlan all = pack_sizes(*c->pool, lens + lo, hi - lo);
+		const size_t mean = std::max<size_t>(
+		    all.start[all.nt] / std::max<uint64_t>(hi - lo, 1), 16);
+		per_chunk = std::max<size_t>(kChunkBytes / mean, 1);
+	}
 	for (uint64_t at = lo; at < hi && rc == 0;) {
-		/* chunk end: at most kChunkBytes of (padded) payload */
 		const double tc0 = dbg_now();
-		uint64_t end = at;
-		size_t bytes = 0;
-		if (offsets == nullptr) {
-			const size_t per = std::max<size_t>(
-			    (fixed_len + 15) & ~15u, 16);
-			end = std::min<uint64_t>(hi, at + std::max<size_t>(
-			    kChunkBytes / per, 1));
-		} else {
-			while (end < hi && (bytes == 0 ||
-			    bytes + lens[end] <= kChunkBytes)) {
-				bytes += ((size_t)lens[end] + 15) & ~(size_t)15;
-				end++;
-			}
-		}
+		const uint64_t end = std::min<uint64_t>(hi, at + per_chunk);
 		Slot &s = c->slot[cur];
 		const double td0 = dbg_now();
 		if ((rc = drain(s)) != 0)
@@ -440,11 +541,11 @@ int run_device_slice(size_t didx, int alg, const uint8_t *base,
 		if (dbg_timing())
 			fprintf(stderr, "net2: drain wait %.3f ms\n", dbg_now() - td0);
 		const double te0 = dbg_now();
-		rc = enqueue_chunk(s, alg, base, offsets, lens, stride,
-		    fixed_len, at, end, bytes, digests + at * dl, src_pinned,
+		rc = enqueue_chunk(*c->pool, s, alg, base, offsets, lens, stride,
+		    fixed_len, at, end, digests + at * dl, src_pinned,
 		    dst_pinned);
 		if (dbg_timing())
-			fprintf(stderr, "net2: enqueue %.3f ms (chunk-end scan %.3f ms)\n",
+			fprintf(stderr, "net2: enqueue %.3f ms (+%.3f ms before it)\n",
 			    dbg_now() - te0, te0 - tc0);
 		at = end;
 		cur ^= 1;

@@ -250,6 +250,28 @@ def test_host_batch_var_multichunk(dev, batch, oracle_mod):
         assert bad.size == 0, bad[:8]
 
 
+def test_host_batch_skewed_chunks(dev, batch, oracle_mod):
+    """Chunks are cut by packet count at the slice's mean size: a run of
+    jumbo packets ahead of many runts puts ~2x kChunkBytes in the first
+    chunk (staging grows to fit).  Also a pageable fixed layout whose stride
+    is not the 16-byte padded length (parallel strided gather, two chunks)."""
+    lens = np.concatenate([np.full(15000, 9000), np.full(150000, 20)]).astype(np.uint32)
+    data, offs = synth.packed(28, lens, align=1, gap=1)
+    got = batch.digest_host(1, data, offsets=offs, lens=lens, max_devices=1)
+    want = oracle_mod.batch(1, data, offsets=offs, lens=lens,
+                            nthreads=CPU_THREADS)
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert bad.size == 0, bad[:8]
+    n, length, stride = 70000, 1000, 1001
+    data = synth.random_bytes(29, (n - 1) * stride + length)
+    got = batch.digest_host(3, data, stride=stride, length=length, n=n,
+                            max_devices=1)
+    want = oracle_mod.batch(3, data, stride=stride, length=length, n=n,
+                            nthreads=CPU_THREADS)
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert bad.size == 0, bad[:8]
+
+
 # ---- BASELINE.json configs at full size ------------------------------------
 
 def _full_fixed(dev, batch, oracle_mod, alg, seed):
