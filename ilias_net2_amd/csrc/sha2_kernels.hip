@@ -507,10 +507,94 @@ __global__ __launch_bounds__(256) void fixed_kernel(const uint8_t *__restrict__ 
 }
 
 /*
+ * K[t] + W[t] of the SHA-256 pad block of every message whose length is a
+ * whole number of blocks, 64 * j bytes for j < NET2_PADTAB_N (up to
+ * 65,536-byte payloads plus an HMAC key block): 0x80, zero fill, bit count
+ * 512 * j (SHA256Pad for usedspace == 0, src/sha2.c:520-526).  Evaluated
+ * at compile time into constant memory, so a wave whose lanes all carry the
+ * same such length reads its pad schedule with scalar loads instead of
+ * expanding it (48 of 64 schedule words, ~480 VALU instructions per lane),
+ * as fixed_kernel does with its kernel-argument copy.
+ */
+#ifndef NET2_PADTAB
+#define NET2_PADTAB 1
+#endif
+#define NET2_PADTAB_N 1026
+
+struct PadTab256 {
+	uint32_t kw[NET2_PADTAB_N][64];
+};
+
+constexpr uint32_t cx_ror32(uint32_t x, int n)
+{
+	return (x >> n) | (x << (32 - n));
+}
+
+constexpr PadTab256 make_padtab256()
+{
+	PadTab256 t{};
+	for (int j = 0; j < NET2_PADTAB_N; j++) {
+		uint32_t w[64] = {};
+		const uint64_t bits = (uint64_t)j * 512;
+		w[0] = 0x80000000u;
+		w[14] = (uint32_t)(bits >> 32);
+		w[15] = (uint32_t)bits;
+		for (int r = 16; r < 64; r++) {
+			const uint32_t s0 = cx_ror32(w[r - 15], 7) ^
+			    cx_ror32(w[r - 15], 18) ^ (w[r - 15] >> 3);
+			const uint32_t s1 = cx_ror32(w[r - 2], 17) ^
+			    cx_ror32(w[r - 2], 19) ^ (w[r - 2] >> 10);
+			w[r] = w[r - 16] + s0 + w[r - 7] + s1;
+		}
+		for (int r = 0; r < 64; r++)
+			t.kw[j][r] = K256[r] + w[r];
+	}
+	return t;
+}
+
+__constant__ const PadTab256 g_padtab256 = make_padtab256();
+
+/*
+ * The wave-uniform pad schedule for messages of `bytes` total bytes (any
+ * prefix included), or nullptr when the wave's live lanes differ in length,
+ * the length is not a whole number of blocks or lies past the table.
+ */
+template <class H>
+__device__ __forceinline__ const typename H::word *uniform_pad_kw(bool live,
+    uint64_t bytes)
+{
+	if (!NET2_PADTAB || sizeof(typename H::word) != 4)
+		return nullptr;
+	const uint32_t lo = (uint32_t)bytes;
+	const uint32_t b0 = __builtin_amdgcn_readfirstlane(lo);
+	if (!__all(!live || bytes == b0) || b0 % 64 != 0 ||
+	    b0 / 64 >= NET2_PADTAB_N)
+		return nullptr;
+	return reinterpret_cast<const typename H::word *>(
+	    g_padtab256.kw[b0 / 64]);
+}
+
+/* digest_one for the variable layout: one block loop, and the pad block
+ * from the constant table when the wave has one (kw != nullptr). */
+template <class H, int AMODE, bool PREFETCH = H::PREFETCH>
+__device__ __forceinline__ void var_digest(const uint8_t *p, uint32_t len,
+    int is384, const typename H::word *kw, typename H::State &st)
+{
+	H::init(st, is384);
+	absorb<H, AMODE, PREFETCH>(p, len, st);
+	if (sizeof(typename H::word) == 4 && kw != nullptr)
+		finish<H, true>(p, len, 0, kw, st);
+	else
+		finish<H, false>(p, len, (uint64_t)len << 3, nullptr, st);
+}
+
+/*
  * Variable-length packets, visited in binned order: lane g hashes packet
  * perm[g] (perm == NULL: identity).  The address mode is chosen per wave:
  * if every lane's packet start is 16-byte aligned the wave takes the vector
- * load path, else the byte-aligned one.
+ * load path, else the byte-aligned one.  A wave of one whole-block length
+ * (a bin of a batch of fixed sizes) takes its pad schedule from
+ * g_padtab256.
  */
 template <class H>
 __global__ __launch_bounds__(256) void var_kernel(const uint8_t *__restrict__ base,
@@ -526,15 +610,16 @@ __global__ __launch_bounds__(256) void var_kernel(const uint8_t *__restrict__ ba
 	const uint8_t *p = base + (live ? offsets[i] : 0);
 	const uint32_t len = live ? lens[i] : 0;
 	typename H::State st;
+	const typename H::word *kw = uniform_pad_kw<H>(live, len);
 
 	if (__all((reinterpret_cast<uintptr_t>(p) & 15) == 0))
-		digest_one<H, AMODE_A16, false>(p, len, is384, nullptr, st);
+		var_digest<H, AMODE_A16>(p, len, is384, kw, st);
 	else if (__all((reinterpret_cast<uintptr_t>(p) & 3) == 0))
-		digest_one<H, AMODE_A4, false>(p, len, is384, nullptr, st);
+		var_digest<H, AMODE_A4>(p, len, is384, kw, st);
 	else
-		digest_one<H, AMODE_A1, false,
-		    H::PREFETCH && NET2_VAR_A1_PREFETCH != 0>(p, len, is384,
-		    nullptr, st);
+		var_digest<H, AMODE_A1,
+		    H::PREFETCH && NET2_VAR_A1_PREFETCH != 0>(p, len, is384, kw,
+		    st);
 	materialize<H>(st);
 	if (!live)
 		return;
@@ -606,28 +691,33 @@ __device__ __forceinline__ void load_mid(const uint32_t (*mid)[16], int which,
 template <class H, int AMODE, bool PADCONST, bool PREFETCH = H::PREFETCH>
 __device__ __forceinline__ void hmac_inner(const uint8_t *p, uint32_t len,
     const uint32_t (*mid)[16], const typename H::word *kw,
-    typename H::State &st)
+    typename H::State &st, bool padtab)
 {
 	load_mid<H>(mid, 0, st);
 	absorb<H, AMODE, PREFETCH>(p, len, st);
-	finish<H, PADCONST>(p, len, ((uint64_t)len + H::BLOCK) << 3, kw, st);
+	if (!PADCONST && sizeof(typename H::word) == 4 && padtab)
+		finish<H, true>(p, len, 0, kw, st);
+	else
+		finish<H, PADCONST>(p, len, ((uint64_t)len + H::BLOCK) << 3, kw,
+		    st);
 }
 
 template <class H, bool PADCONST>
 __device__ __forceinline__ void hmac_lane(const uint8_t *p, uint32_t len,
     int is384, int amode, const uint32_t (*mid)[16],
-    const typename H::word *kw, typename H::State &st)
+    const typename H::word *kw, typename H::State &st, bool padtab = false)
 {
 	constexpr int NW32 = H::NW32;
 	/* the midstates stay in LDS and are read where they are used, so
 	 * neither is held in VGPRs across the block loop */
 	if (amode == AMODE_A16)
-		hmac_inner<H, AMODE_A16, PADCONST>(p, len, mid, kw, st);
+		hmac_inner<H, AMODE_A16, PADCONST>(p, len, mid, kw, st, padtab);
 	else if (amode == AMODE_A4)
-		hmac_inner<H, AMODE_A4, PADCONST>(p, len, mid, kw, st);
+		hmac_inner<H, AMODE_A4, PADCONST>(p, len, mid, kw, st, padtab);
 	else
 		hmac_inner<H, AMODE_A1, PADCONST,
-		    H::PREFETCH && NET2_HMAC_A1_PREFETCH != 0>(p, len, mid, kw, st);
+		    H::PREFETCH && NET2_HMAC_A1_PREFETCH != 0>(p, len, mid, kw, st,
+		    padtab);
 
 	/* outer: one block = inner digest || 0x80 || 0... || bit count */
 	uint32_t w[NW32];
@@ -726,7 +816,14 @@ __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ b
 	const uintptr_t pa = reinterpret_cast<uintptr_t>(p);
 	const int amode = __all((pa & 15) == 0) ? AMODE_A16 :
 	    __all((pa & 3) == 0) ? AMODE_A4 : AMODE_A1;
-	hmac_lane<H, PADCONST>(p, len, is384, amode, mid, pad.kw, st);
+	/* a variable-layout wave of one whole-block inner length (key block
+	 * included) takes its inner pad schedule from g_padtab256 */
+	const typename H::word *kw = nullptr;
+	if constexpr (!PADCONST && sizeof(typename H::word) == 4)
+		if (offsets != nullptr)
+			kw = uniform_pad_kw<H>(live, (uint64_t)len + H::BLOCK);
+	hmac_lane<H, PADCONST>(p, len, is384, amode, mid,
+	    kw != nullptr ? kw : pad.kw, st, kw != nullptr);
 	materialize<H>(st);
 	if (!live)
 		return;

@@ -202,6 +202,38 @@ def test_var_permuted_offsets(dev, batch, oracle_mod):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("align", [16, 4, 1])
+def test_var_whole_block_lengths(dev, batch, oracle_mod, align):
+    """Waves whose lanes share one whole-block length read the pad block's
+    schedule from the kernel's constant table (g_padtab256): both ends of the
+    table (0 and 65,600 bytes), one past it, in each address mode (16-byte,
+    4-byte and byte-aligned packet starts), for SHA-256 digests and
+    HMAC-SHA256 (inner length = key block + message)."""
+    js = (0, 1, 2, 8, 1023, 1024, 1025, 1026)
+    lens = np.repeat(np.array([64 * j for j in js], dtype=np.uint32), 70)
+    lens = np.concatenate([lens, np.array([64, 60, 0, 3], dtype=np.uint32)])
+    data, offs = synth.packed(77 + align, lens, align=align,
+                              gap={16: 0, 4: 4, 1: 1}[align])
+    dt = to_dev(data, dev)
+    do = to_dev(offs.astype(np.int64), dev)
+    dl = to_dev(lens.astype(np.int32), dev)
+    want = oracle_mod.batch(1, data, offsets=offs, lens=lens,
+                            nthreads=CPU_THREADS)
+    for binned in (True, False):
+        got = batch.digest_var(1, dt, do, dl, binned=binned).cpu().numpy()
+        bad = np.nonzero((got != want).any(axis=1))[0]
+        assert bad.size == 0, (binned, lens[bad[:8]])
+    key = bytes(synth.random_bytes(78, 32))
+    want = np.stack([np.frombuffer(oracle_mod.hmac(
+        4, key, data[int(o):int(o) + int(l)].tobytes()), dtype=np.uint8)
+        for o, l in zip(offs, lens)])
+    for binned in (True, False):
+        got = batch.hmac_dev(4, key, dt, offsets=do, lens=dl,
+                             binned=binned).cpu().numpy()
+        bad = np.nonzero((got != want).any(axis=1))[0]
+        assert bad.size == 0, (binned, lens[bad[:8]])
+
+
 # ---- host-memory end-to-end path (net2_sha2_batch) ------------------------
 
 def test_host_batch(dev, batch, oracle_mod):
