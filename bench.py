@@ -35,6 +35,10 @@ CONFIGS = {
                workload="1M x mixed {64,512,1500} B packets, SHA-256, length-binned (configs[2])"),
     "c4": dict(alg=3, kind="fixed", n=1 << 20, length=1024,
                workload="1M x 1 KiB packets, SHA-512, device-resident (configs[3])"),
+    # the negotiated sighash (SHA-512) over variable-length payloads: the
+    # signed-carver flow's shape (not a BASELINE config)
+    "c3_512": dict(alg=3, kind="mixed", n=1 << 20, length=None,
+                   workload="1M x mixed {64,512,1500} B packets, SHA-512, length-binned"),
     # SURVEY.md 8f rows, for DESIGN.md (not BASELINE configs)
     "hmac": dict(alg=4, kind="fixed", n=1 << 20, length=1024,
                  workload="1M x 1 KiB packets, HMAC-SHA256, device-resident (8f row 1)"),

@@ -574,15 +574,81 @@ __device__ __forceinline__ const typename H::word *uniform_pad_kw(bool live,
 	    g_padtab256.kw[b0 / 64]);
 }
 
+/*
+ * The SHA-512 counterpart: K[t] + W[t] of the pad block of a 128 * j byte
+ * message (0x80, zeros, 128-bit bit count 1024 * j; SHA512Pad,
+ * src/sha2.c:784-832) for j < NET2_PADTAB512_N, 329 KB of constant memory.
+ * SHA-512 compressions read their round constants from the workgroup's LDS
+ * copy (k512_lds, NET2_KM512), so the table row is staged there, in the
+ * [80, 160) half the fixed kernel's constant pad block uses; that makes the
+ * choice per workgroup: every live lane of it must share the length.
+ */
+#define NET2_PADTAB512_N 514
+
+struct PadTab512 {
+	uint64_t kw[NET2_PADTAB512_N][80];
+};
+
+constexpr uint64_t cx_ror64(uint64_t x, int n)
+{
+	return (x >> n) | (x << (64 - n));
+}
+
+constexpr PadTab512 make_padtab512()
+{
+	PadTab512 t{};
+	for (int j = 0; j < NET2_PADTAB512_N; j++) {
+		uint64_t w[80] = {};
+		w[0] = 0x8000000000000000ull;
+		w[15] = (uint64_t)j * 1024;	/* w[14]: high half of the count */
+		for (int r = 16; r < 80; r++) {
+			const uint64_t s0 = cx_ror64(w[r - 15], 1) ^
+			    cx_ror64(w[r - 15], 8) ^ (w[r - 15] >> 7);
+			const uint64_t s1 = cx_ror64(w[r - 2], 19) ^
+			    cx_ror64(w[r - 2], 61) ^ (w[r - 2] >> 6);
+			w[r] = w[r - 16] + s0 + w[r - 7] + s1;
+		}
+		for (int r = 0; r < 80; r++)
+			t.kw[j][r] = K512[r] + w[r];
+	}
+	return t;
+}
+
+__constant__ const PadTab512 g_padtab512 = make_padtab512();
+
+/*
+ * Workgroup-uniform whole-block length for SHA-512: stage its pad schedule
+ * in k512_lds[80, 160) and return true.  Called by every thread of the
+ * workgroup (it synchronises), after k512_lds_fill().
+ */
+__device__ __forceinline__ bool block_pad512(bool live, uint64_t bytes)
+{
+	if (!NET2_PADTAB)
+		return false;
+	__shared__ uint64_t b0s;
+	if (threadIdx.x == 0)
+		b0s = live ? bytes : 1;	/* thread 0 is live if any thread is */
+	__syncthreads();
+	const uint64_t b0 = b0s;
+	const bool same = __syncthreads_and(!live || bytes == b0);
+	if (!same || b0 % 128 != 0 || b0 / 128 >= NET2_PADTAB512_N)
+		return false;
+	for (unsigned t = threadIdx.x; t < 80; t += blockDim.x)
+		k512_lds[80 + t] = g_padtab512.kw[b0 / 128][t];
+	__syncthreads();
+	return true;
+}
+
 /* digest_one for the variable layout: one block loop, and the pad block
- * from the constant table when the wave has one (kw != nullptr). */
+ * from the constant table when the wave (SHA-256: kw) or the workgroup
+ * (SHA-512: k512_lds) has one. */
 template <class H, int AMODE, bool PREFETCH = H::PREFETCH>
 __device__ __forceinline__ void var_digest(const uint8_t *p, uint32_t len,
-    int is384, const typename H::word *kw, typename H::State &st)
+    int is384, const typename H::word *kw, bool padtab, typename H::State &st)
 {
 	H::init(st, is384);
 	absorb<H, AMODE, PREFETCH>(p, len, st);
-	if (sizeof(typename H::word) == 4 && kw != nullptr)
+	if (padtab)
 		finish<H, true>(p, len, 0, kw, st);
 	else
 		finish<H, false>(p, len, (uint64_t)len << 3, nullptr, st);
@@ -611,15 +677,18 @@ __global__ __launch_bounds__(256) void var_kernel(const uint8_t *__restrict__ ba
 	const uint32_t len = live ? lens[i] : 0;
 	typename H::State st;
 	const typename H::word *kw = uniform_pad_kw<H>(live, len);
+	bool padtab = kw != nullptr;
+	if constexpr (sizeof(typename H::word) == 8)
+		padtab = block_pad512(live, len);
 
 	if (__all((reinterpret_cast<uintptr_t>(p) & 15) == 0))
-		var_digest<H, AMODE_A16>(p, len, is384, kw, st);
+		var_digest<H, AMODE_A16>(p, len, is384, kw, padtab, st);
 	else if (__all((reinterpret_cast<uintptr_t>(p) & 3) == 0))
-		var_digest<H, AMODE_A4>(p, len, is384, kw, st);
+		var_digest<H, AMODE_A4>(p, len, is384, kw, padtab, st);
 	else
 		var_digest<H, AMODE_A1,
 		    H::PREFETCH && NET2_VAR_A1_PREFETCH != 0>(p, len, is384, kw,
-		    st);
+		    padtab, st);
 	materialize<H>(st);
 	if (!live)
 		return;
@@ -695,7 +764,7 @@ __device__ __forceinline__ void hmac_inner(const uint8_t *p, uint32_t len,
 {
 	load_mid<H>(mid, 0, st);
 	absorb<H, AMODE, PREFETCH>(p, len, st);
-	if (!PADCONST && sizeof(typename H::word) == 4 && padtab)
+	if (!PADCONST && padtab)
 		finish<H, true>(p, len, 0, kw, st);
 	else
 		finish<H, PADCONST>(p, len, ((uint64_t)len + H::BLOCK) << 3, kw,
@@ -816,14 +885,24 @@ __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ b
 	const uintptr_t pa = reinterpret_cast<uintptr_t>(p);
 	const int amode = __all((pa & 15) == 0) ? AMODE_A16 :
 	    __all((pa & 3) == 0) ? AMODE_A4 : AMODE_A1;
-	/* a variable-layout wave of one whole-block inner length (key block
-	 * included) takes its inner pad schedule from g_padtab256 */
+	/* a variable-layout wave (SHA-256) or workgroup (SHA-512) of one
+	 * whole-block inner length (key block included) takes its inner pad
+	 * schedule from g_padtab256 / g_padtab512 */
 	const typename H::word *kw = nullptr;
-	if constexpr (!PADCONST && sizeof(typename H::word) == 4)
+	bool padtab = false;
+	if constexpr (!PADCONST && sizeof(typename H::word) == 4) {
 		if (offsets != nullptr)
 			kw = uniform_pad_kw<H>(live, (uint64_t)len + H::BLOCK);
+		padtab = kw != nullptr;
+	} else if constexpr (!PADCONST && MODE != HMAC_VERIFY) {
+		/* SHA-512: per workgroup, staged in k512_lds (block_pad512); the
+		 * RX verify kernel measured 0.5 % slower with it
+		 * (profiles/round1/padtab512_ab.txt) */
+		if (offsets != nullptr)
+			padtab = block_pad512(live, (uint64_t)len + H::BLOCK);
+	}
 	hmac_lane<H, PADCONST>(p, len, is384, amode, mid,
-	    kw != nullptr ? kw : pad.kw, st, kw != nullptr);
+	    kw != nullptr ? kw : pad.kw, st, padtab);
 	materialize<H>(st);
 	if (!live)
 		return;

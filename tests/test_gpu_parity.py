@@ -202,36 +202,44 @@ def test_var_permuted_offsets(dev, batch, oracle_mod):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("alg", [1, 3])
 @pytest.mark.parametrize("align", [16, 4, 1])
-def test_var_whole_block_lengths(dev, batch, oracle_mod, align):
-    """Waves whose lanes share one whole-block length read the pad block's
-    schedule from the kernel's constant table (g_padtab256): both ends of the
-    table (0 and 65,600 bytes), one past it, in each address mode (16-byte,
-    4-byte and byte-aligned packet starts), for SHA-256 digests and
-    HMAC-SHA256 (inner length = key block + message)."""
-    js = (0, 1, 2, 8, 1023, 1024, 1025, 1026)
-    lens = np.repeat(np.array([64 * j for j in js], dtype=np.uint32), 70)
-    lens = np.concatenate([lens, np.array([64, 60, 0, 3], dtype=np.uint32)])
+def test_var_whole_block_lengths(dev, batch, oracle_mod, alg, align):
+    """Lanes that share one whole-block length read the pad block's schedule
+    from the kernels' constant tables (g_padtab256 per wave, g_padtab512 per
+    workgroup): both ends of each table, one past it, in each address mode
+    (16-byte, 4-byte and byte-aligned packet starts), for the digests and the
+    HMAC rows (inner length = key block + message)."""
+    if alg == 1:
+        blk, js, copies = 64, (0, 1, 2, 8, 1023, 1024, 1025, 1026), 70
+    else:   # whole 256-lane workgroups of one length
+        blk, js, copies = 128, (0, 1, 2, 8, 511, 512, 513, 514), 520
+    lens = np.repeat(np.array([blk * j for j in js], dtype=np.uint32), copies)
+    lens = np.concatenate([lens, np.array([blk, blk - 4, 0, 3], dtype=np.uint32)])
     data, offs = synth.packed(77 + align, lens, align=align,
                               gap={16: 0, 4: 4, 1: 1}[align])
     dt = to_dev(data, dev)
     do = to_dev(offs.astype(np.int64), dev)
     dl = to_dev(lens.astype(np.int32), dev)
-    want = oracle_mod.batch(1, data, offsets=offs, lens=lens,
+    want = oracle_mod.batch(alg, data, offsets=offs, lens=lens,
                             nthreads=CPU_THREADS)
     for binned in (True, False):
-        got = batch.digest_var(1, dt, do, dl, binned=binned).cpu().numpy()
+        got = batch.digest_var(alg, dt, do, dl, binned=binned).cpu().numpy()
         bad = np.nonzero((got != want).any(axis=1))[0]
         assert bad.size == 0, (binned, lens[bad[:8]])
-    key = bytes(synth.random_bytes(78, 32))
+    halg = alg + 3
+    key = bytes(synth.random_bytes(78, DLEN_OF[halg]))
     want = np.stack([np.frombuffer(oracle_mod.hmac(
-        4, key, data[int(o):int(o) + int(l)].tobytes()), dtype=np.uint8)
+        halg, key, data[int(o):int(o) + int(l)].tobytes()), dtype=np.uint8)
         for o, l in zip(offs, lens)])
     for binned in (True, False):
-        got = batch.hmac_dev(4, key, dt, offsets=do, lens=dl,
+        got = batch.hmac_dev(halg, key, dt, offsets=do, lens=dl,
                              binned=binned).cpu().numpy()
         bad = np.nonzero((got != want).any(axis=1))[0]
         assert bad.size == 0, (binned, lens[bad[:8]])
+
+
+DLEN_OF = {4: 32, 5: 48, 6: 64}
 
 
 # ---- host-memory end-to-end path (net2_sha2_batch) ------------------------
