@@ -28,7 +28,8 @@ import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = {"c2": "fixed_kernel<net2::dev::Sha256", "c4": "fixed_kernel<net2::dev::Sha512",
-          "c3": "var_kernel<net2::dev::Sha256", "hmac": "hmac_kernel<net2::dev::Sha256",
+          "c3": "var_kernel<net2::dev::Sha256", "c3_512": "var_kernel<net2::dev::Sha512",
+          "hmac": "hmac_kernel<net2::dev::Sha256",
           "hmac_mtu": "hmac_kernel<net2::dev::Sha256", "ph_iv": "ph_iv_kernel",
           "hmac512": "hmac_kernel<net2::dev::Sha512", "hmac512_mtu": "hmac_kernel<net2::dev::Sha512"}
 
