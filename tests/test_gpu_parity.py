@@ -202,7 +202,7 @@ def test_var_permuted_offsets(dev, batch, oracle_mod):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("alg", [1, 3])
+@pytest.mark.parametrize("alg", [1, 2, 3])
 @pytest.mark.parametrize("align", [16, 4, 1])
 def test_var_whole_block_lengths(dev, batch, oracle_mod, alg, align):
     """Lanes that share one whole-block length read the pad block's schedule
@@ -212,7 +212,7 @@ def test_var_whole_block_lengths(dev, batch, oracle_mod, alg, align):
     HMAC rows (inner length = key block + message)."""
     if alg == 1:
         blk, js, copies = 64, (0, 1, 2, 8, 1023, 1024, 1025, 1026), 70
-    else:   # whole 256-lane workgroups of one length
+    else:   # SHA-384/512: whole 256-lane workgroups of one length
         blk, js, copies = 128, (0, 1, 2, 8, 511, 512, 513, 514), 520
     lens = np.repeat(np.array([blk * j for j in js], dtype=np.uint32), copies)
     lens = np.concatenate([lens, np.array([blk, blk - 4, 0, 3], dtype=np.uint32)])
