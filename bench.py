@@ -109,6 +109,15 @@ def _cpu_model():
     return None
 
 
+def _smt_active():
+    """SMT state of the host (SURVEY.md 8(d) asks for it), or None."""
+    try:
+        with open("/sys/devices/system/cpu/smt/active") as f:
+            return f.read().strip() == "1"
+    except OSError:
+        return None
+
+
 def cpu_baseline(cfg):
     """Oracle (clean-room C restatement of src/sha2.c, -O3) on host cores."""
     import numpy as np
@@ -146,6 +155,9 @@ def cpu_baseline(cfg):
     single = n1 / (time.perf_counter() - t0)
     return {"value": n / best, "unit": "digests/s", "cores": threads,
             "single_thread_value": single, "cpu_model": _cpu_model(),
+            "host_cpus": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0)),
+            "smt_active": _smt_active(),
             "kind": "port",
             "sample": (f"the full {cfg['workload'].split(' packets')[0]} packet batch from host memory, "
                        f"oracle/sha2_oracle.c (-O3, rolled transform like src/sha2.c:374-445) "
