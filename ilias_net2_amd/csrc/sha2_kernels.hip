@@ -658,9 +658,9 @@ __device__ __forceinline__ void var_digest(const uint8_t *p, uint32_t len,
  * Variable-length packets, visited in binned order: lane g hashes packet
  * perm[g] (perm == NULL: identity).  The address mode is chosen per wave:
  * if every lane's packet start is 16-byte aligned the wave takes the vector
- * load path, else the byte-aligned one.  A wave of one whole-block length
- * (a bin of a batch of fixed sizes) takes its pad schedule from
- * g_padtab256.
+ * load path, else the byte-aligned one.  A SHA-256 wave (SHA-512:
+ * workgroup) of one whole-block length, e.g. a bin of a batch of fixed
+ * sizes, takes its pad schedule from g_padtab256 (g_padtab512).
  */
 template <class H>
 __global__ __launch_bounds__(256) void var_kernel(const uint8_t *__restrict__ base,
