@@ -826,6 +826,12 @@ __device__ __forceinline__ void hmac_lane(const uint8_t *p, uint32_t len,
  */
 enum { HMAC_DIGESTS = 0, HMAC_SIGN = 1, HMAC_VERIFY = 2 };
 
+/* VERIFY: compare the hash field in whole words when the wave's message
+ * starts (and so its hash fields) are 4- or 16-byte aligned */
+#ifndef NET2_VERIFY_WORDS
+#define NET2_VERIFY_WORDS 1
+#endif
+
 template <class H, bool PADCONST, int MODE = HMAC_DIGESTS>
 __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ base,
     const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
@@ -894,10 +900,8 @@ __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ b
 		if (offsets != nullptr)
 			kw = uniform_pad_kw<H>(live, (uint64_t)len + H::BLOCK);
 		padtab = kw != nullptr;
-	} else if constexpr (!PADCONST && MODE != HMAC_VERIFY) {
-		/* SHA-512: per workgroup, staged in k512_lds (block_pad512); the
-		 * RX verify kernel measured 0.5 % slower with it
-		 * (profiles/round1/padtab512_ab.txt) */
+	} else if constexpr (!PADCONST) {
+		/* SHA-512: per workgroup, staged in k512_lds (block_pad512) */
 		if (offsets != nullptr)
 			padtab = block_pad512(live, (uint64_t)len + H::BLOCK);
 	}
@@ -912,8 +916,33 @@ __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ b
 		/* o[] holds the digest bytes little-endian per word, the order
 		 * store_digest writes them in */
 		uint32_t diff = 0;
-		for (uint32_t j = 0; j < dlen && !short_dgram; j++)
-			diff |= field[j] ^ ((o[j >> 2] >> (8 * (j & 3))) & 0xffu);
+		constexpr int NO = H::DLEN / 4;	/* dlen / 4 <= NO (SHA-384: 12) */
+		if (!short_dgram && NET2_VERIFY_WORDS && amode == AMODE_A16) {
+			/* field = message start - dlen: 16-byte aligned as well;
+			 * all loads issued at once (a per-byte loop waited out one
+			 * memory latency per byte) */
+			const u32x4 *f = reinterpret_cast<const u32x4 *>(field);
+#pragma unroll
+			for (int k = 0; k < NO / 4; k++)
+				if (16 * k < (int)dlen) {
+					const u32x4 v = f[k];
+					diff |= (v.x ^ o[4 * k]) | (v.y ^ o[4 * k + 1]) |
+					    (v.z ^ o[4 * k + 2]) | (v.w ^ o[4 * k + 3]);
+				}
+		} else if (!short_dgram && NET2_VERIFY_WORDS &&
+		    amode == AMODE_A4) {
+			const uint32_t *f = reinterpret_cast<const uint32_t *>(field);
+#pragma unroll
+			for (int k = 0; k < NO; k++)
+				if (4 * k < (int)dlen)
+					diff |= f[k] ^ o[k];
+		} else if (!short_dgram) {
+#pragma unroll
+			for (int j = 0; j < 4 * NO; j++)
+				if (j < (int)dlen)
+					diff |= field[j] ^
+					    ((o[j >> 2] >> (8 * (j & 3))) & 0xffu);
+		}
 		out[i] = short_dgram ? 2 : diff != 0;
 		return;
 	}
