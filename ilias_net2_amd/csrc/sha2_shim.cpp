@@ -108,6 +108,25 @@ const std::vector<int> &devices()
 	return g_devices;
 }
 
+/*
+ * Devices a host-memory batch (net2_sha2_batch) is sharded over.  Test
+ * knob NET2_SHA2_VIRTUAL_DEVICES=k (read per call): every real device is
+ * listed k times, so each entry gets its own DeviceCtx, stream pair and
+ * host thread and the multi-device slicing runs on a one-GPU machine.
+ */
+std::vector<int> batch_devices()
+{
+	std::vector<int> dv = devices();
+	const char *v = getenv("NET2_SHA2_VIRTUAL_DEVICES");
+	const int k = v != nullptr ? atoi(v) : 1;
+	if (k > 1 && k <= 64 && !dv.empty()) {
+		const std::vector<int> real = dv;
+		for (int r = 1; r < k; r++)
+			dv.insert(dv.end(), real.begin(), real.end());
+	}
+	return dv;
+}
+
 /* Is the calling thread's current device one we built code for? */
 int check_current_device()
 {
@@ -163,8 +182,12 @@ struct Slot {
 		cap_in = cap_n = 0;
 	}
 
-	/* Grow to hold `in` payload bytes and `n` packets. */
-	int reserve(size_t in, size_t n)
+	/*
+	 * Grow to hold `in` payload bytes and `n` packets.  host_in == false:
+	 * the payload is DMA'd straight from the caller's pinned memory, so
+	 * no pinned input staging is allocated (or kept) for it.
+	 */
+	int reserve(size_t in, size_t n, bool host_in = true)
 	{
 		if (stream == nullptr) {
 			HIP_TRY(hipStreamCreateWithFlags(&stream,
@@ -172,7 +195,7 @@ struct Slot {
 			HIP_TRY(hipEventCreateWithFlags(&done,
 			    hipEventDisableTiming));
 		}
-		if (in <= cap_in && n <= cap_n)
+		if (in <= cap_in && n <= cap_n && (!host_in || h_in != nullptr))
 			return 0;
 		/* grow both dimensions monotonically, with headroom: chunks of a
 		 * variable-length batch differ slightly in bytes and packet count,
@@ -181,7 +204,9 @@ struct Slot {
 		in = std::max<size_t>({in + in / 8, cap_in, 4096});
 		n = std::max<size_t>({n + n / 4, cap_n, 64});
 		release();
-		HIP_TRY(hipHostMalloc((void **)&h_in, in, hipHostMallocDefault));
+		if (host_in)
+			HIP_TRY(hipHostMalloc((void **)&h_in, in,
+			    hipHostMallocDefault));
 		HIP_TRY(hipHostMalloc((void **)&h_dig, n * 64,
 		    hipHostMallocDefault));
 		HIP_TRY(hipHostMalloc((void **)&h_off, n * 8,
@@ -308,8 +333,8 @@ std::vector<std::unique_ptr<DeviceCtx>> g_ctx;
 DeviceCtx *ctx_for(size_t idx)
 {
 	std::lock_guard<std::mutex> g(g_ctx_mu);
-	if (g_ctx.size() < devices().size())
-		g_ctx.resize(devices().size());
+	if (g_ctx.size() <= idx)
+		g_ctx.resize(idx + 1);
 	if (!g_ctx[idx])
 		g_ctx[idx].reset(new DeviceCtx());
 	return g_ctx[idx].get();
@@ -334,6 +359,8 @@ void par_memcpy(WorkPool &pool, uint8_t *dst, const uint8_t *src,
     size_t bytes)
 {
 	const size_t piece = 8u << 20;
+	if (bytes == 0)		/* n empty packets at stride 0 */
+		return;
 	const size_t nt = std::min<size_t>(8, (bytes + piece - 1) / piece);
 	pool.run(nt, [=](size_t t) {
 		const size_t a = bytes * t / nt, b = bytes * (t + 1) / nt;
@@ -435,14 +462,15 @@ int enqueue_chunk(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
 		bytes = plan.start[plan.nt];
 	}
 	const double tr0 = dbg_now();
-	if ((rc = s.reserve(bytes, n)) != 0)
+	if ((rc = s.reserve(bytes, n, !(offsets == nullptr && src_pinned))) != 0)
 		return rc;
 	if (dbg_timing())
 		fprintf(stderr, "net2: reserve %.3f ms\n", dbg_now() - tr0);
 
 	if (offsets == nullptr && src_pinned) {
-		HIP_TRY(hipMemcpyAsync(s.d_in, base + lo * stride, bytes,
-		    hipMemcpyHostToDevice, s.stream));
+		if (bytes != 0)
+			HIP_TRY(hipMemcpyAsync(s.d_in, base + lo * stride,
+			    bytes, hipMemcpyHostToDevice, s.stream));
 		HIP_TRY(net2_launch_fixed(alg, s.d_in, stride, fixed_len, n,
 		    s.d_dig, s.stream));
 	} else if (offsets == nullptr) {
@@ -463,8 +491,9 @@ int enqueue_chunk(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
 					    fixed_len);
 			});
 		}
-		HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
-		    hipMemcpyHostToDevice, s.stream));
+		if (bytes != 0)
+			HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
+			    hipMemcpyHostToDevice, s.stream));
 		HIP_TRY(net2_launch_fixed(alg, s.d_in, st, fixed_len, n,
 		    s.d_dig, s.stream));
 	} else {
@@ -474,8 +503,9 @@ int enqueue_chunk(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
 		if (dbg_timing())
 			fprintf(stderr, "net2: pack %zu B, %llu packets: %.3f ms\n",
 			    bytes, (unsigned long long)n, dbg_now() - tg0);
-		HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
-		    hipMemcpyHostToDevice, s.stream));
+		if (bytes != 0)
+			HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
+			    hipMemcpyHostToDevice, s.stream));
 		HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, n * 8,
 		    hipMemcpyHostToDevice, s.stream));
 		HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, n * 4,
@@ -504,7 +534,7 @@ int drain(Slot &s)
 }
 
 /* One device's share of a host-memory batch. */
-int run_device_slice(size_t didx, int alg, const uint8_t *base,
+int run_device_slice(size_t didx, int ordinal, int alg, const uint8_t *base,
     const uint64_t *offsets, const uint32_t *lens, uint64_t stride,
     uint32_t fixed_len, uint64_t lo, uint64_t hi, uint8_t *digests)
 {
@@ -513,7 +543,7 @@ int run_device_slice(size_t didx, int alg, const uint8_t *base,
 	const int dl = digest_len(alg);
 	int rc = 0, cur = 0;
 
-	HIP_TRY(hipSetDevice(devices()[didx]));
+	HIP_TRY(hipSetDevice(ordinal));
 	const bool src_pinned = offsets == nullptr && is_pinned(base);
 	const bool dst_pinned = is_pinned(digests);
 	/*
@@ -523,7 +553,11 @@ int run_device_slice(size_t didx, int alg, const uint8_t *base,
 	 */
 	uint64_t per_chunk;
 	if (offsets == nullptr) {
-		const size_t per = std::max<size_t>((fixed_len + 15) & ~15u, 16);
+		/* the direct-DMA path copies whole strides (a chunk spans
+		 * (n - 1) * stride + fixed_len bytes), the staged one packs
+		 * packets at 16-byte granularity */
+		const size_t per = std::max<size_t>(src_pinned ? stride :
+		    (fixed_len + 15) & ~15u, 16);
 		per_chunk = std::max<size_t>(kChunkBytes / per, 1);
 	} else {
 		const PackPlan all = pack_sizes(*c->pool, lens + lo, hi - lo);
@@ -704,7 +738,7 @@ NET2_EXPORT int net2_sha2_batch(int alg, const void *base,
 		return EINVAL;
 	if (offsets == nullptr && n > 1 && stride < fixed_len)
 		return EINVAL;
-	const std::vector<int> &dv = devices();
+	const std::vector<int> dv = batch_devices();
 	if (dv.empty())
 		return ENODEV;
 	size_t nd = dv.size();
@@ -745,12 +779,14 @@ NET2_EXPORT int net2_sha2_batch(int alg, const void *base,
 	std::vector<std::thread> th;
 	for (size_t d = 1; d < nd; d++)
 		th.emplace_back([&, d]() {
-			rcs[d] = run_device_slice((first + d) % dv.size(), alg,
+			const size_t e = (first + d) % dv.size();
+			rcs[d] = run_device_slice(e, dv[e], alg,
 			    (const uint8_t *)base, offsets, lens, stride,
 			    fixed_len, cut[d], cut[d + 1], (uint8_t *)digests);
 		});
-	rcs[0] = run_device_slice(first, alg, (const uint8_t *)base, offsets,
-	    lens, stride, fixed_len, cut[0], cut[1], (uint8_t *)digests);
+	rcs[0] = run_device_slice(first, dv[first], alg, (const uint8_t *)base,
+	    offsets, lens, stride, fixed_len, cut[0], cut[1],
+	    (uint8_t *)digests);
 	for (std::thread &t : th)
 		t.join();
 	if (prev >= 0)

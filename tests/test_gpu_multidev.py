@@ -1,0 +1,240 @@
+"""The host-memory batch path (net2_sha2_batch) over several devices, and the
+stream-ordered lifetime of the Python wrappers' temporaries.
+
+net2_sha2_batch cuts a batch into contiguous slices (by packet count, or by
+bytes for the variable layout) and runs one host thread + stream pair per
+device (one host thread per device; the reference's callers
+are threadpool workers, include/ilias/net2/threadpool.h:33-34).  The test box
+has one GPU, so NET2_SHA2_VIRTUAL_DEVICES=k lists it k times: every slice gets
+its own DeviceCtx, staging slots, streams and thread, exactly as on an
+8-GPU node, and the cut / device-walk / digest-placement code runs for k > 1.
+Every digest is compared with the oracle.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import synth
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+CPU_THREADS = min(16, len(os.sched_getaffinity(0)))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a GPU (HIP device not visible)")
+    from ilias_net2_amd import _lib
+    assert _lib.device_count() >= 1
+    return torch.device("cuda:0")
+
+
+@pytest.fixture
+def virtual(monkeypatch):
+    def set_k(k):
+        monkeypatch.setenv("NET2_SHA2_VIRTUAL_DEVICES", str(k))
+    yield set_k
+
+
+def _bad(got, want):
+    return np.nonzero((got != want).any(axis=1))[0][:8]
+
+
+@pytest.mark.parametrize("k", [2, 3, 8])
+def test_fixed_pageable_and_pinned(dev, virtual, oracle_mod, k):
+    from ilias_net2_amd import _lib, batch
+    virtual(k)
+    n, length, stride = 50001, 700, 704
+    data = synth.random_bytes(100 + k, (n - 1) * stride + length)
+    want = oracle_mod.batch(1, data, stride=stride, length=length, n=n,
+                            nthreads=CPU_THREADS)
+    got = batch.digest_host(1, data, stride=stride, length=length, n=n,
+                            max_devices=k)
+    assert _bad(got, want).size == 0, _bad(got, want)
+    # pinned source and destination: direct DMA per slice
+    src = torch.from_numpy(data).pin_memory()
+    out = torch.zeros((n, 32), dtype=torch.uint8).pin_memory()
+    assert _lib.lib().net2_sha2_batch(1, src.data_ptr(), None, None, stride,
+                                      length, n, out.data_ptr(), k) == 0
+    assert _bad(out.numpy(), want).size == 0
+    # SHA-384 digests land at 48-byte spacing across slice boundaries
+    got = batch.digest_host(2, data, stride=stride, length=length, n=n,
+                            max_devices=k)
+    assert np.array_equal(got, oracle_mod.batch(2, data, stride=stride,
+                                                length=length, n=n,
+                                                nthreads=CPU_THREADS))
+
+
+@pytest.mark.parametrize("k", [2, 3, 8])
+def test_var_byte_balanced(dev, virtual, oracle_mod, k):
+    from ilias_net2_amd import batch
+    virtual(k)
+    lens = synth.mixed_lengths(200 + k, 40000, choices=(64, 512, 1500, 0, 9000))
+    data, offs = synth.packed(201 + k, lens, align=1, gap=2)
+    for alg in (1, 3):
+        want = oracle_mod.batch(alg, data, offsets=offs, lens=lens,
+                                nthreads=CPU_THREADS)
+        got = batch.digest_host(alg, data, offsets=offs, lens=lens,
+                                max_devices=k)
+        assert _bad(got, want).size == 0, (alg, _bad(got, want))
+
+
+def test_fewer_packets_than_devices(dev, virtual, oracle_mod):
+    from ilias_net2_amd import batch
+    virtual(8)
+    for n in (1, 3, 7):
+        data = synth.fixed_batch(300 + n, n, 1024)
+        got = batch.digest_host(3, data, stride=1024, length=1024, n=n,
+                                max_devices=8)
+        assert np.array_equal(got, oracle_mod.batch(3, data, stride=1024,
+                                                    length=1024, n=n))
+        lens = np.array([5, 70000, 3, 1, 0, 129, 64][:n], dtype=np.uint32)
+        vdata, offs = synth.packed(310 + n, lens)
+        got = batch.digest_host(1, vdata, offsets=offs, lens=lens, max_devices=8)
+        assert np.array_equal(got, oracle_mod.batch(1, vdata, offsets=offs,
+                                                    lens=lens))
+
+
+def test_cut_on_jumbo_packet(dev, virtual, oracle_mod):
+    """One packet holds most of the bytes: the byte-balanced cuts of several
+    devices all land on it, leaving empty slices."""
+    from ilias_net2_amd import batch
+    virtual(8)
+    lens = np.full(5001, 40, dtype=np.uint32)
+    lens[2500] = 3_000_000
+    data, offs = synth.packed(320, lens, align=1)
+    want = oracle_mod.batch(1, data, offsets=offs, lens=lens)
+    got = batch.digest_host(1, data, offsets=offs, lens=lens, max_devices=8)
+    assert _bad(got, want).size == 0
+    got = batch.digest_host(3, data, offsets=offs, lens=lens, max_devices=3)
+    assert np.array_equal(got, oracle_mod.batch(3, data, offsets=offs, lens=lens))
+
+
+def test_empty_packets_stride_zero(dev, oracle_mod):
+    """n empty messages at stride 0 (the header allows stride >= fixed_len):
+    every digest is the empty-message digest, pageable and pinned."""
+    from ilias_net2_amd import _lib
+    n = 1000
+    empty = oracle_mod.digest(1, b"")
+    out = np.zeros((n, 32), dtype=np.uint8)
+    one = np.zeros(1, dtype=np.uint8)
+    assert _lib.lib().net2_sha2_batch(1, one.ctypes.data, None, None, 0, 0, n,
+                                      out.ctypes.data, 1) == 0
+    assert all(r.tobytes() == empty for r in out)
+    out[:] = 0
+    assert _lib.lib().net2_sha2_batch(1, None, None, None, 0, 0, n,
+                                      out.ctypes.data, 1) == 0
+    assert all(r.tobytes() == empty for r in out)
+    pin = torch.zeros(16, dtype=torch.uint8).pin_memory()
+    out[:] = 0
+    assert _lib.lib().net2_sha2_batch(1, pin.data_ptr(), None, None, 0, 0, n,
+                                      out.ctypes.data, 1) == 0
+    assert all(r.tobytes() == empty for r in out)
+
+
+def test_pinned_sparse_records(dev, oracle_mod):
+    """64-byte records in 4 KiB slots of pinned memory: direct-DMA chunks are
+    sized by the stride (a chunk sized by the record length would span
+    ~16x the staging target)."""
+    from ilias_net2_amd import _lib
+    n, length, stride = 40000, 64, 4096
+    src = torch.from_numpy(synth.random_bytes(330, (n - 1) * stride + length)).pin_memory()
+    out = np.zeros((n, 64), dtype=np.uint8)
+    assert _lib.lib().net2_sha2_batch(3, src.data_ptr(), None, None, stride,
+                                      length, n, out.ctypes.data, 1) == 0
+    want = oracle_mod.batch(3, src.numpy(), stride=stride, length=length, n=n,
+                            nthreads=CPU_THREADS)
+    assert _bad(out, want).size == 0
+
+
+# ---- stream-ordered temporaries (ilias_net2_amd/batch.py) -------------------
+
+def _clobber(dev, nbytes, rounds=4):
+    """Allocate and overwrite memory on the current stream: if a wrapper had
+    freed a temporary that a side-stream kernel still reads, the caching
+    allocator would hand it out here."""
+    keep = []
+    for _ in range(rounds):
+        t = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        t.fill_(0xA5)
+        keep.append(t)
+    return keep
+
+
+def test_side_stream_temporaries(dev, oracle_mod):
+    from ilias_net2_amd import batch
+    n = 200000
+    lens = synth.mixed_lengths(340, n, choices=(64, 512, 1500, 9000))
+    data, offs = synth.packed(341, lens, align=4)
+    d = torch.from_numpy(data).to(dev)
+    o = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    ln = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    key = bytes(range(32))
+    ws_bytes = (2 * 2048 + n) * 4
+    side = torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    side.wait_stream(torch.cuda.current_stream(dev))
+    got = batch.digest_var(1, d, o, ln, stream=side)     # temp workspace
+    keep = _clobber(dev, ws_bytes)
+    got_h = batch.hmac_dev(4, key, d, offsets=o, lens=ln, stream=side)
+    keep += _clobber(dev, ws_bytes)
+    side.synchronize()
+    torch.cuda.synchronize()
+    want = oracle_mod.batch(1, data, offsets=offs, lens=lens,
+                            nthreads=CPU_THREADS)
+    assert np.array_equal(got.cpu().numpy(), want)
+    hm = got_h.cpu().numpy()
+    for i in range(0, n, 997):
+        m = data[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes()
+        assert hm[i].tobytes() == oracle_mod.hmac(4, key, m), i
+    del keep
+
+
+def test_hmac_graph_capture(dev, oracle_mod):
+    """The HMAC wrappers synchronise nothing, so binned HMAC, datagram sign
+    and verify launches can be captured into a hipGraph and replayed."""
+    from ilias_net2_amd import batch
+    n = 4000
+    lens = synth.mixed_lengths(350, n, choices=(64, 512, 1500, 100))
+    data, offs = synth.packed(351, lens, align=16)
+    d = torch.from_numpy(data).to(dev)
+    o = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    ln = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    key = bytes(range(64))
+    out = torch.zeros((n, 64), dtype=torch.uint8, device=dev)
+    res = torch.full((n,), 9, dtype=torch.uint8, device=dev)
+    s = torch.cuda.Stream(dev)
+    ws = batch.var_workspace(n, dev, s)
+    signed = d.clone()
+    with torch.cuda.stream(s):
+        batch.hmac_dev(6, key, d, offsets=o, lens=ln, out=out, stream=s,
+                       workspace=ws)
+        batch.hmac_sign_dev(6, key, signed, o, ln, stream=s, workspace=ws)
+        batch.hmac_verify_dev(6, key, signed, o, ln, stream=s, out=res,
+                              workspace=ws)
+    torch.cuda.synchronize()
+    out.zero_()
+    res.fill_(9)
+    signed.copy_(d)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        batch.hmac_dev(6, key, d, offsets=o, lens=ln, out=out, stream=s,
+                       workspace=ws)
+        batch.hmac_sign_dev(6, key, signed, o, ln, stream=s, workspace=ws)
+        batch.hmac_verify_dev(6, key, signed, o, ln, stream=s, out=res,
+                              workspace=ws)
+    g.replay()
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    sg = signed.cpu().numpy()
+    for i in range(n):
+        m = data[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes()
+        assert got[i].tobytes() == oracle_mod.hmac(6, key, m), i
+        if lens[i] >= 64:
+            field = sg[int(offs[i]):int(offs[i]) + 64].tobytes()
+            assert field == oracle_mod.hmac(6, key, m[64:]), i
+    r = res.cpu().numpy()
+    assert np.array_equal(r, np.where(lens >= 64, 0, 2).astype(np.uint8))
