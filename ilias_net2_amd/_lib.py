@@ -1,7 +1,7 @@
 """ctypes binding of libnet2_sha2.so, the C-ABI of the MI355X SHA-2 path.
 
-The binding declares exactly the entry points of include/net2/sha2_batch.h and
-include/net2/hash.h.  Loading is strict: if the shared library is missing the
+The binding declares exactly the entry points of include/net2/sha2_batch.h,
+include/net2/hash.h, include/net2/packet.h and include/net2/sha2.h.  Loading is strict: if the shared library is missing the
 import of any compute helper raises, there is no Python or CPU fallback.
 """
 from __future__ import annotations
@@ -79,7 +79,23 @@ SIGNATURES = {
     "net2_ph_to_iv_dev": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
         ctypes.c_void_p, ctypes.c_void_p]),
+    # include/net2/sha2.h: the streaming interface of src/sha2.c
+    "net2_sha2_ctx_init": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p]),
+    "net2_sha2_ctx_update": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_size_t]),
+    "net2_sha2_ctx_pad": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p]),
+    "net2_sha2_ctx_final": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_void_p]),
+    "net2_sha2_ctx_transform": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p,
+                                               ctypes.c_void_p]),
 }
+for _pfx in ("SHA256", "SHA384", "SHA512"):
+    SIGNATURES[_pfx + "Init"] = (None, [ctypes.c_void_p])
+    SIGNATURES[_pfx + "Update"] = (None, [ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_size_t])
+    SIGNATURES[_pfx + "Pad"] = (None, [ctypes.c_void_p])
+    SIGNATURES[_pfx + "Final"] = (None, [ctypes.c_void_p, ctypes.c_void_p])
+    SIGNATURES[_pfx + "Transform"] = (None, [ctypes.c_void_p, ctypes.c_void_p])
 DATA_SYMBOLS = ("net2_hashmax",)
 
 _lib = None

@@ -1,0 +1,510 @@
+/*
+ * sha2_coalesce.cpp -- request coalescer for the single-message paths
+ * (see sha2_coalesce.h).
+ *
+ * Per device: a few batch slots, each with pinned host staging, device
+ * staging, a stream and an event.  One slot at a time is "open": callers
+ * reserve a range of its staging under the device mutex, copy and pad their
+ * message outside it, and wait.  The first caller of a batch leads it:
+ *   - it launches at once if no other batch of this device is in flight
+ *     (an idle GPU: lowest latency for a lone caller),
+ *   - otherwise when the batch is full or the batching window (default
+ *     40 us, NET2_COALESCE_WINDOW_US) has passed since it opened -- the
+ *     callers that arrive while earlier batches run share one launch;
+ * then it waits for the batch's event (spinning briefly, then blocking) and
+ * hands every caller its result.  Several batches may be in flight at once
+ * (NET2_COALESCE_SLOTS, default 4), each on its own stream.
+ *
+ * Layout of a batch in staging: every job's blocks (the message already
+ * padded as SHA*Pad would, src/sha2.c:495-543 / :784-832, behind the
+ * K' ^ ipad block for HMAC), then its aux block (K' ^ opad, or the state to
+ * continue from), each job 64-byte aligned; at launch the leader appends
+ * the job descriptors.  Results: 64 bytes of raw state per job.
+ */
+#include "sha2_coalesce.h"
+#include "sha2_launch.h"
+
+#include <hip/hip_runtime.h>
+
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+namespace net2co {
+namespace {
+
+typedef std::chrono::steady_clock clk;
+
+constexpr int kMaxSlots = 16;
+constexpr size_t kInitialStage = 1u << 20;	/* grows on demand */
+constexpr size_t kMaxJobs = 1u << 16;		/* per batch */
+
+int env_int(const char *name, int dflt, int lo, int hi)
+{
+	const char *v = getenv(name);
+	if (v == nullptr || *v == '\0')
+		return dflt;
+	return std::min(hi, std::max(lo, atoi(v)));
+}
+
+size_t align64(size_t x)
+{
+	return (x + 63) & ~(size_t)63;
+}
+
+struct Job {
+	Net2Job desc;		/* offsets relative to the slot's staging */
+	int kind, alg;
+	uint8_t *out;
+	bool done = false;
+	int rc = 0;
+	int hip = 0;		/* HIP error behind rc == EIO */
+};
+
+struct Slot {
+	hipStream_t stream = nullptr;
+	hipEvent_t ev = nullptr;
+	uint8_t *h_stage = nullptr, *d_stage = nullptr;
+	size_t cap = 0;
+	uint8_t *h_out = nullptr, *d_out = nullptr;
+	size_t cap_jobs = 0;
+	/* the batch being filled or run */
+	std::vector<Job *> jobs;
+	size_t used = 0;
+	int writers = 0;
+	bool full = false;
+	clk::time_point opened;
+
+	void free_stage()
+	{
+		if (h_stage) (void)hipHostFree(h_stage);
+		if (d_stage && d_stage != h_stage) (void)hipFree(d_stage);
+		h_stage = d_stage = nullptr;
+		cap = 0;
+	}
+	void free_out()
+	{
+		if (h_out) (void)hipHostFree(h_out);
+		if (d_out && d_out != h_out) (void)hipFree(d_out);
+		h_out = d_out = nullptr;
+		cap_jobs = 0;
+	}
+};
+
+/*
+ * zerocopy: the kernel reads the staging and writes the results through
+ * the host mappings of coherent pinned buffers, so a batch costs one kernel
+ * launch and no copy; otherwise staging is copied to device memory and the
+ * results back.
+ */
+hipError_t host_alloc(uint8_t **p, size_t bytes, bool zerocopy)
+{
+	return hipHostMalloc((void **)p, bytes, zerocopy ?
+	    (hipHostMallocMapped | hipHostMallocCoherent) : hipHostMallocDefault);
+}
+
+class Coalescer {
+public:
+	Coalescer()
+	    : nslots_(env_int("NET2_COALESCE_SLOTS", 4, 1, kMaxSlots)),
+	      window_(std::chrono::microseconds(
+		  env_int("NET2_COALESCE_WINDOW_US", 40, 0, 100000))),
+	      zerocopy_(env_int("NET2_COALESCE_ZEROCOPY", 0, 0, 1) != 0)
+	{
+		for (int i = nslots_ - 1; i >= 0; i--)
+			free_.push_back(i);
+	}
+
+	int submit(int ordinal, const Request &r, int *hip_err);
+
+private:
+	int grow_stage(Slot &s, size_t need, int ordinal);
+	int launch_and_wait(Slot &s, int ordinal, int *hip_err);
+
+	std::mutex mu_;
+	std::condition_variable cv_;
+	Slot slot_[kMaxSlots];
+	const int nslots_;
+	const clk::duration window_;
+	const bool zerocopy_;
+	int open_ = -1;
+	std::vector<int> free_;
+	int inflight_ = 0;
+};
+
+int Coalescer::grow_stage(Slot &s, size_t need, int ordinal)
+{
+	/* only for an empty open batch, with the device mutex held; device
+	 * memory goes on `ordinal`, whatever the caller's current device */
+	int prev = -1;
+	(void)hipGetDevice(&prev);
+	struct Restore {
+		int dev;
+		~Restore() { if (dev >= 0) (void)hipSetDevice(dev); }
+	} restore = { prev };
+	if (hipSetDevice(ordinal) != hipSuccess)
+		return EIO;
+	size_t cap = std::max(kInitialStage, need + need / 4);
+	s.free_stage();
+	uint8_t *h = nullptr, *d = nullptr;
+	if (host_alloc(&h, cap, zerocopy_) != hipSuccess)
+		return ENOMEM;
+	if (zerocopy_) {
+		if (hipHostGetDevicePointer((void **)&d, h, 0) != hipSuccess) {
+			(void)hipHostFree(h);
+			return ENOMEM;
+		}
+	} else if (hipMalloc((void **)&d, cap) != hipSuccess) {
+		(void)hipHostFree(h);
+		return ENOMEM;
+	}
+	s.h_stage = h;
+	s.d_stage = d;
+	s.cap = cap;
+	return 0;
+}
+
+size_t iov_total(const struct iovec *iov, size_t n)
+{
+	size_t t = 0;
+	for (size_t i = 0; i < n; i++)
+		t += iov[i].iov_len;
+	return t;
+}
+
+uint8_t *gather(uint8_t *dst, const struct iovec *iov, size_t n)
+{
+	for (size_t i = 0; i < n; i++) {
+		if (iov[i].iov_len)
+			memcpy(dst, iov[i].iov_base, iov[i].iov_len);
+		dst += iov[i].iov_len;
+	}
+	return dst;
+}
+
+/* Bytes of a padded message of `len` bytes: 0x80, zeros, the 64-bit
+ * (SHA-256) or 128-bit (SHA-384/512) big-endian bit count. */
+size_t padded_len(size_t len, size_t blk)
+{
+	const size_t lenbytes = blk == 64 ? 8 : 16;
+	return (len + 1 + lenbytes + blk - 1) / blk * blk;
+}
+
+/* Terminator, zero fill and bit count after `len` message bytes at p
+ * (which starts the padded message of padded_len(len) bytes). */
+void put_pad(uint8_t *p, size_t len, size_t blk, uint64_t bits)
+{
+	const size_t total = padded_len(len, blk);
+	p[len] = 0x80;
+	memset(p + len + 1, 0, total - len - 1);
+	for (int i = 0; i < 8; i++)
+		p[total - 1 - i] = (uint8_t)(bits >> (8 * i));
+}
+
+void key_block(uint8_t *p, const uint8_t *key, size_t keylen, size_t blk,
+    uint8_t pad)
+{
+	for (size_t i = 0; i < blk; i++)
+		p[i] = (uint8_t)((i < keylen ? key[i] : 0) ^ pad);
+}
+
+int Coalescer::submit(int ordinal, const Request &r, int *hip_err)
+{
+	const size_t blk = r.alg == 1 ? 64 : 128;
+	const size_t msg = iov_total(r.iov, r.iovcnt);
+	size_t body, aux;
+
+	switch (r.kind) {
+	case DIGEST:
+		body = padded_len(msg, blk);
+		aux = 0;
+		break;
+	case HMAC:
+		if (r.keylen > blk)
+			return EINVAL;
+		body = padded_len(blk + msg, blk);
+		aux = blk;
+		break;
+	case BLOCKS:
+		if (msg % blk != 0 || r.state == nullptr)
+			return EINVAL;
+		body = msg;
+		aux = 64;
+		break;
+	default:
+		return EINVAL;
+	}
+	const size_t need = align64(body + aux);
+	const size_t nblk = body / blk;
+	if (nblk > UINT32_MAX)
+		return EINVAL;
+
+	Job job;
+	job.kind = r.kind;
+	job.alg = r.alg;
+	job.out = r.out;
+	std::unique_lock<std::mutex> lk(mu_);
+	Slot *sp;
+	int si;
+	for (;;) {
+		if (open_ < 0) {
+			if (free_.empty()) {
+				cv_.wait(lk);
+				continue;
+			}
+			open_ = free_.back();
+			free_.pop_back();
+			Slot &s = slot_[open_];
+			s.jobs.clear();
+			s.used = 0;
+			s.writers = 0;
+			s.full = false;
+			s.opened = clk::now();
+		}
+		Slot &s = slot_[open_];
+		const size_t hdr = (s.jobs.size() + 1) * sizeof(Net2Job);
+		if (s.used + need + hdr <= s.cap && s.jobs.size() < kMaxJobs)
+			break;
+		if (s.jobs.empty()) {
+			int rc = grow_stage(s, need + hdr, ordinal);
+			if (rc != 0)
+				return rc;
+			continue;
+		}
+		/* no room: the leader launches it now; join the next batch */
+		s.full = true;
+		const int cur = open_;
+		cv_.notify_all();
+		cv_.wait(lk, [&]() { return open_ != cur; });
+	}
+	si = open_;
+	sp = &slot_[si];
+	Slot &s = *sp;
+	const size_t off = s.used;
+	s.used += need;
+	s.jobs.push_back(&job);
+	s.writers++;
+	const bool leader = s.jobs.size() == 1;
+	if (!leader && s.used + 2 * 1024 > s.cap)
+		s.full = true;
+	lk.unlock();
+
+	/* lay the job out in staging (no lock: the range is ours) */
+	uint8_t *p = s.h_stage + off;
+	job.desc.data = off;
+	job.desc.aux = off + body;
+	job.desc.nblk = (uint32_t)nblk;
+	job.desc.flags = (uint32_t)r.alg;
+	if (r.kind == DIGEST) {
+		gather(p, r.iov, r.iovcnt);
+		put_pad(p, msg, blk, (uint64_t)msg << 3);
+	} else if (r.kind == HMAC) {
+		key_block(p, r.key, r.keylen, blk, 0x36);
+		gather(p + blk, r.iov, r.iovcnt);
+		put_pad(p, blk + msg, blk, (uint64_t)(blk + msg) << 3);
+		key_block(p + body, r.key, r.keylen, blk, 0x5c);
+		job.desc.flags |= NET2_JOB_HMAC;
+	} else {
+		gather(p, r.iov, r.iovcnt);
+		memcpy(p + body, r.state, blk == 64 ? 32 : 64);
+		job.desc.flags |= NET2_JOB_STATE;
+	}
+
+	lk.lock();
+	if (--s.writers == 0)
+		cv_.notify_all();
+	if (!leader) {
+		cv_.wait(lk, [&]() { return job.done; });
+		if (job.rc == EIO && hip_err != nullptr)
+			*hip_err = job.hip;
+		return job.rc;
+	}
+
+	/* leader: launch when the device is idle, the batch full, or the
+	 * window over */
+	cv_.wait_until(lk, s.opened + window_, [&]() {
+		return inflight_ == 0 || s.full;
+	});
+	if (open_ == si)
+		open_ = -1;		/* later callers open the next batch */
+	cv_.wait(lk, [&]() { return s.writers == 0; });
+	inflight_++;
+	cv_.notify_all();		/* callers waiting for a new open batch */
+	lk.unlock();
+
+	int herr = 0;
+	const int rc = launch_and_wait(s, ordinal, &herr);
+	if (rc == EIO && hip_err != nullptr)
+		*hip_err = herr;
+
+	lk.lock();
+	for (Job *jp : s.jobs) {
+		jp->rc = rc;
+		jp->hip = herr;
+		jp->done = true;
+	}
+	s.jobs.clear();
+	inflight_--;
+	free_.push_back(si);
+	cv_.notify_all();
+	return rc;
+}
+
+void store_be32(uint8_t *p, uint32_t v)
+{
+	p[0] = (uint8_t)(v >> 24);
+	p[1] = (uint8_t)(v >> 16);
+	p[2] = (uint8_t)(v >> 8);
+	p[3] = (uint8_t)v;
+}
+
+/* Raw state words -> the caller's output (digest bytes as SHA*Final
+ * stores them, src/sha2.c:553-557 / :847-850 / :905-908, or the state). */
+void deliver(const Job &j, const uint8_t *raw)
+{
+	if (j.kind == BLOCKS) {
+		memcpy(j.out, raw, j.alg == 1 ? 32 : 64);
+		return;
+	}
+	if (j.alg == 1) {
+		uint32_t w[8];
+		memcpy(w, raw, sizeof(w));
+		for (int i = 0; i < 8; i++)
+			store_be32(j.out + 4 * i, w[i]);
+		return;
+	}
+	uint64_t w[8];
+	memcpy(w, raw, sizeof(w));
+	for (int i = 0; i < (j.alg == 2 ? 6 : 8); i++) {
+		store_be32(j.out + 8 * i, (uint32_t)(w[i] >> 32));
+		store_be32(j.out + 8 * i + 4, (uint32_t)w[i]);
+	}
+}
+
+int Coalescer::launch_and_wait(Slot &s, int ordinal, int *hip_err)
+{
+	int prev = -1;
+	(void)hipGetDevice(&prev);
+	struct Restore {
+		int dev;
+		~Restore() { if (dev >= 0) (void)hipSetDevice(dev); }
+	} restore = { prev };
+	hipError_t e;
+#define CO_TRY(expr)                                                         \
+	do {                                                                 \
+		if ((e = (expr)) != hipSuccess)                              \
+			goto fail;                                           \
+	} while (0)
+
+	std::vector<Job *> &jobs = s.jobs;
+	const size_t n = jobs.size();
+	size_t hdr_off, n256;
+	const uint8_t *stage;
+	const Net2Job *descs;
+	uint8_t *out;
+
+	CO_TRY(hipSetDevice(ordinal));
+	if (s.stream == nullptr) {
+		CO_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+		CO_TRY(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+	}
+	if (s.cap_jobs < n) {
+		const size_t want = std::max<size_t>(n + n / 2, 256);
+		s.free_out();
+		CO_TRY(host_alloc(&s.h_out, want * 64, zerocopy_));
+		if (zerocopy_)
+			CO_TRY(hipHostGetDevicePointer((void **)&s.d_out, s.h_out, 0));
+		else
+			CO_TRY(hipMalloc((void **)&s.d_out, want * 64));
+		s.cap_jobs = want;
+	}
+	/* SHA-256 jobs first, then SHA-384/512; longest first within each,
+	 * so a wave's lanes share their trip count as far as possible */
+	std::sort(jobs.begin(), jobs.end(), [](const Job *a, const Job *b) {
+		const int fa = a->alg != 1, fb = b->alg != 1;
+		if (fa != fb)
+			return fa < fb;
+		return a->desc.nblk > b->desc.nblk;
+	});
+	hdr_off = align64(s.used);
+	n256 = 0;
+	for (size_t k = 0; k < n; k++) {
+		memcpy(s.h_stage + hdr_off + k * sizeof(Net2Job), &jobs[k]->desc,
+		    sizeof(Net2Job));
+		n256 += jobs[k]->alg == 1;
+	}
+	if (zerocopy_) {
+		stage = s.d_stage;
+	} else {
+		CO_TRY(hipMemcpyAsync(s.d_stage, s.h_stage,
+		    hdr_off + n * sizeof(Net2Job), hipMemcpyHostToDevice,
+		    s.stream));
+		stage = s.d_stage;
+	}
+	descs = reinterpret_cast<const Net2Job *>(stage + hdr_off);
+	out = s.d_out;
+	CO_TRY(net2_launch_jobs(stage, descs, (uint32_t)n256,
+	    (uint32_t)(n - n256), out, s.stream));
+	if (!zerocopy_)
+		CO_TRY(hipMemcpyAsync(s.h_out, s.d_out, n * 64,
+		    hipMemcpyDeviceToHost, s.stream));
+	CO_TRY(hipEventRecord(s.ev, s.stream));
+	{
+		/* a small batch finishes in tens of microseconds: spin on the
+		 * event (a blocking wait adds a wake-up), then block */
+		const clk::time_point t0 = clk::now();
+		for (;;) {
+			e = hipEventQuery(s.ev);
+			if (e != hipErrorNotReady)
+				break;
+			if (clk::now() - t0 > std::chrono::milliseconds(2)) {
+				e = hipEventSynchronize(s.ev);
+				break;
+			}
+			__builtin_ia32_pause();
+		}
+		if (e != hipSuccess)
+			goto fail;
+	}
+	for (size_t k = 0; k < n; k++)
+		deliver(*jobs[k], s.h_out + 64 * k);
+	return 0;
+fail:
+	if (hip_err != nullptr)
+		*hip_err = (int)e;
+	(void)hipGetLastError();
+	return e == hipErrorOutOfMemory ? ENOMEM : EIO;
+#undef CO_TRY
+}
+
+std::mutex g_mu;
+std::vector<std::unique_ptr<Coalescer>> g_co;
+
+Coalescer *coalescer(size_t idx)
+{
+	std::lock_guard<std::mutex> g(g_mu);
+	if (g_co.size() <= idx)
+		g_co.resize(idx + 1);
+	if (!g_co[idx])
+		g_co[idx].reset(new Coalescer());
+	return g_co[idx].get();
+}
+
+}	/* namespace */
+
+int submit(size_t idx, int ordinal, const Request &r, int *hip_err)
+{
+	if (r.alg < 1 || r.alg > 3 || (r.iovcnt > 0 && r.iov == nullptr) ||
+	    r.out == nullptr)
+		return EINVAL;
+	return coalescer(idx)->submit(ordinal, r, hip_err);
+}
+
+}	/* namespace net2co */

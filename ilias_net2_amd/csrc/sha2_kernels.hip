@@ -957,6 +957,69 @@ __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ b
 		store_digest<64>(dst, o);
 }
 
+/* ---- coalesced small jobs (sha2_coalesce.cpp) ------------------------------- */
+
+/*
+ * One lane = one request of the single-message entry points
+ * (net2_hashctx_hashiov, the SHA2_CTX streaming calls, net2_ph_to_iv), which
+ * the reference runs one payload at a time on threadpool workers
+ * (types/signature.n2t:92,147, src/sign.c:298-307, types/packet.n2t:134-142).
+ * Concurrent requests are gathered by the host into one staging buffer,
+ * every message already padded to whole blocks (SHA*Pad's layout, or the
+ * K' ^ ipad block ahead of it for HMAC), so a lane only compresses.
+ */
+template <class H>
+__global__ __launch_bounds__(64) void job_kernel(const uint8_t *__restrict__ stage,
+    const Net2Job *__restrict__ jobs, uint32_t n, uint8_t *__restrict__ out)
+{
+	constexpr int NW32 = H::NW32;
+	typedef typename H::word W;
+	if (sizeof(W) == 8)
+		k512_lds_fill();
+	const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+	if (j >= n)
+		return;
+	const Net2Job jb = jobs[j];
+	const int is384 = (jb.flags & 0xffu) == NET2_ALG_SHA384;
+	typename H::State st;
+	if (jb.flags & NET2_JOB_STATE) {
+		const W *s0 = reinterpret_cast<const W *>(stage + jb.aux);
+#pragma unroll
+		for (int i = 0; i < 8; i++)
+			st[i] = s0[i];
+	} else {
+		H::init(st, is384);
+	}
+	absorb<H, AMODE_A16>(stage + jb.data, jb.nblk * (uint32_t)H::BLOCK, st);
+	if (jb.flags & NET2_JOB_HMAC) {
+		/* outer hash: IV, K' ^ opad, inner digest || 0x80 || bit count */
+		uint32_t w[NW32];
+#pragma unroll
+		for (int i = 0; i < NW32; i++)
+			w[i] = 0;
+		const int dw = digest_words<H>(st, is384, w);
+#pragma unroll
+		for (int i = 12; i < 16; i++)		/* SHA-384 keeps 12 words */
+			if (i >= dw)
+				w[i] = 0;
+		w[dw] = 0x80000000u;
+		const uint64_t obits = (uint64_t)(H::BLOCK + 4 * dw) << 3;
+		w[NW32 - 2] = (uint32_t)(obits >> 32);
+		w[NW32 - 1] = (uint32_t)obits;
+		H::init(st, is384);
+		Raw<NW32> r;
+		issue_block<NW32, AMODE_A16>(stage + jb.aux, r);
+		uint32_t kb[NW32];
+		finish_block<NW32, AMODE_A16>(stage + jb.aux, r, kb);
+		H::compress(st, kb);
+		H::compress(st, w);
+	}
+	W *o = reinterpret_cast<W *>(out + 64 * (size_t)j);
+#pragma unroll
+	for (int i = 0; i < 8; i++)
+		o[i] = st[i];
+}
+
 /* ---- packet-header IV derivation (types/packet.n2t:100-158) ---------------- */
 
 /*
@@ -1459,6 +1522,19 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 	}
 	return hipGetLastError();
 }
+hipError_t net2_launch_jobs(const uint8_t *stage, const Net2Job *jobs,
+    uint32_t n256, uint32_t n512, uint8_t *out, hipStream_t s)
+{
+	/* 64-lane workgroups: a few jobs spread over as many CUs as waves */
+	if (n256 > 0)
+		job_kernel<Sha256><<<(n256 + 63) / 64, 64, 0, s>>>(stage, jobs,
+		    n256, out);
+	if (n512 > 0)
+		job_kernel<Sha512><<<(n512 + 63) / 64, 64, 0, s>>>(stage,
+		    jobs + n256, n512, out + 64 * (size_t)n256);
+	return hipGetLastError();
+}
+
 hipError_t net2_launch_ph_iv(const uint32_t *seq, const uint32_t *flags,
     uint64_t n, uint32_t ivlen, uint8_t *out, hipStream_t s)
 {

@@ -52,6 +52,27 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
     uint64_t stride, uint32_t fixed_len, uint64_t n, uint8_t *out,
     uint32_t *ws, hipStream_t s, int mode = NET2_HMAC_MODE_DIGESTS);
 
+/*
+ * Coalesced small jobs (sha2_coalesce.cpp): many independent requests from
+ * host threads, each already laid out by the host as whole blocks in one
+ * staging buffer.  Job j: nblk blocks at stage + data, compressed from the
+ * IV of `alg` (1..3) or, with NET2_JOB_STATE, from the raw state words at
+ * stage + aux; NET2_JOB_HMAC finishes with the outer hash over the
+ * K' ^ opad block at stage + aux.  The final state goes to out + 64 * j as
+ * raw words (uint32_t[8] or uint64_t[8], host byte order).
+ */
+#define NET2_JOB_STATE 0x100u
+#define NET2_JOB_HMAC 0x200u
+struct Net2Job {
+	uint64_t data;
+	uint64_t aux;
+	uint32_t nblk;
+	uint32_t flags;		/* alg | NET2_JOB_* */
+};
+/* jobs [0, n256) are SHA-256, [n256, n256 + n512) SHA-384/512. */
+hipError_t net2_launch_jobs(const uint8_t *stage, const Net2Job *jobs,
+    uint32_t n256, uint32_t n512, uint8_t *out, hipStream_t s);
+
 /* Packet-header IVs (ivlen <= 64): out = n x ivlen bytes. */
 hipError_t net2_launch_ph_iv(const uint32_t *seq, const uint32_t *flags,
     uint64_t n, uint32_t ivlen, uint8_t *out, hipStream_t s);

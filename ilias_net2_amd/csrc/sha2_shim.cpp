@@ -11,6 +11,7 @@
  * fallback.
  */
 #include "sha2_launch.h"
+#include "sha2_coalesce.h"
 
 #include <hip/hip_runtime.h>
 
@@ -323,8 +324,6 @@ struct DeviceCtx {
 	WorkPool *pool = new WorkPool();	/* never freed, see WorkPool */
 	std::mutex mu;		/* one host-memory batch per device at a time */
 	Slot slot[2];
-	Slot small;		/* single-message path (hashiov, HMAC keys) */
-	std::mutex small_mu;
 };
 
 std::mutex g_ctx_mu;
@@ -589,60 +588,33 @@ int run_device_slice(size_t didx, int ordinal, int alg, const uint8_t *base,
 	return rc ? rc : rc2 ? rc2 : rc3;
 }
 
-/* Single message, gathered from iovecs, on the calling thread's current
+/* The device a single-message call runs on: the calling thread's current
  * device when it is a usable one (one process per GPU stays on its GPU),
- * else on the first. */
-int hash_small(int alg, const uint8_t *key, size_t keylen,
-    const struct iovec *iov, size_t iovcnt, uint8_t *out)
+ * else the first. */
+size_t small_device(const std::vector<int> &dv)
 {
-	size_t total = 0;
-	for (size_t i = 0; i < iovcnt; i++)
-		total += iov[i].iov_len;
-	if (total > UINT32_MAX)
-		return EINVAL;
-	int prev = -1;
-	(void)hipGetDevice(&prev);
-	const std::vector<int> &dv = devices();
-	size_t didx = 0;
+	int cur = -1;
+	(void)hipGetDevice(&cur);
 	for (size_t d = 0; d < dv.size(); d++)
-		if (dv[d] == prev)
-			didx = d;
-	DeviceCtx *c = ctx_for(didx);
-	std::lock_guard<std::mutex> g(c->small_mu);
-	HIP_TRY(hipSetDevice(dv[didx]));
-	/* the caller's current device is restored on every return below */
-	struct Restore {
-		int dev;
-		~Restore() { if (dev >= 0) (void)hipSetDevice(dev); }
-	} restore = { prev };
-	Slot &s = c->small;
-	int rc = s.reserve(total, 1);
-	if (rc != 0)
-		return rc;
-	size_t at = 0;
-	for (size_t i = 0; i < iovcnt; i++) {
-		if (iov[i].iov_len)
-			memcpy(s.h_in + at, iov[i].iov_base, iov[i].iov_len);
-		at += iov[i].iov_len;
-	}
-	const int dl = digest_len(alg);
-	HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, std::max<size_t>(total, 1),
-	    hipMemcpyHostToDevice, s.stream));
-	if (unkeyed_sha2(alg))
-		HIP_TRY(net2_launch_fixed(alg, s.d_in, std::max<size_t>(total, 16),
-		    (uint32_t)total, 1, s.d_dig, s.stream));
-	else
-		HIP_TRY(net2_launch_hmac(alg, key, keylen, s.d_in, nullptr,
-		    nullptr, std::max<size_t>(total, 16), (uint32_t)total, 1,
-		    s.d_dig, nullptr, s.stream));
-	HIP_TRY(hipMemcpyAsync(s.h_dig, s.d_dig, dl, hipMemcpyDeviceToHost,
-	    s.stream));
-	HIP_TRY(hipStreamSynchronize(s.stream));
-	memcpy(out, s.h_dig, dl);
+		if (dv[d] == cur)
+			return d;
 	return 0;
 }
 
 } /* namespace */
+
+int net2_co_run(const net2co::Request &r)
+{
+	const std::vector<int> &dv = devices();
+	if (dv.empty())
+		return ENODEV;
+	const size_t d = small_device(dv);
+	int herr = 0;
+	const int rc = net2co::submit(d, dv[d], r, &herr);
+	if (rc == EIO)
+		tl_last_hip_error = herr;
+	return rc;
+}
 
 /* ---- exported C ABI ---------------------------------------------------- */
 
@@ -836,10 +808,16 @@ NET2_EXPORT int net2_hashctx_hashiov(int alg, const void *key, size_t keylen,
 		return 0;
 	if (out == nullptr || outlen < (size_t)kRows[alg].hashlen)
 		return EINVAL;
-	if (devices().empty())
-		return ENODEV;
-	return hash_small(alg, (const uint8_t *)key, keylen, iov, iovcnt,
-	    (uint8_t *)out);
+	/* one coalesced request: concurrent callers share a launch */
+	net2co::Request r = {};
+	r.kind = unkeyed_sha2(alg) ? net2co::DIGEST : net2co::HMAC;
+	r.alg = unkeyed_sha2(alg) ? alg : alg - 3;
+	r.iov = iov;
+	r.iovcnt = iovcnt;
+	r.key = (const uint8_t *)key;
+	r.keylen = keylen;
+	r.out = (uint8_t *)out;
+	return net2_co_run(r);
 }
 
 /* Argument checks shared by the datagram sign / verify entry points. */

@@ -16,10 +16,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_symbols():
     names = set()
-    for hdr in ("sha2_batch.h", "hash.h", "packet.h"):
+    for hdr in ("sha2_batch.h", "hash.h", "packet.h", "sha2.h"):
         src = open(os.path.join(ROOT, "include", "net2", hdr)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-        names.update(re.findall(r"\b(net2_\w+)\s*\(", src))
+        src = re.sub(r"^#.*$", "", src, flags=re.M)
+        names.update(re.findall(r"\b((?:net2_|SHA(?:256|384|512))\w+)\s*\(", src))
         names.update(re.findall(r"extern\s+const\s+int\s+(net2_\w+)\s*;", src))
     return names
 
@@ -34,7 +35,8 @@ def test_every_declared_symbol_exported():
     L = _lib.lib()
     decl = declared_symbols()
     assert {"net2_sha2_dev_fixed", "net2_sha2_dev_var", "net2_sha2_batch",
-            "net2_hashctx_hashiov", "net2_hashmax"} <= decl
+            "net2_hashctx_hashiov", "net2_hashmax", "SHA256Init",
+            "SHA512Transform", "net2_sha2_ctx_update"} <= decl
     for name in decl:
         assert hasattr(L, name), name
     # and the binding declares them all
@@ -108,6 +110,19 @@ def test_argument_errors_without_launch():
     assert L.net2_hashctx_hashiov(99, None, 0, iov, 1, buf, 64) == errno.EINVAL
     # nil hashes to nothing
     assert L.net2_hashctx_hashiov(0, None, 0, iov, 1, None, 0) == 0
+    # streaming context: bad rows, NULL context (Init(NULL) is a no-op,
+    # src/sha2.c:283), zero-length update is a no-op (:455)
+    ctx = ctypes.create_string_buffer(208)
+    assert L.net2_sha2_ctx_init(0, ctx) == errno.EINVAL
+    assert L.net2_sha2_ctx_init(4, ctx) == errno.EINVAL
+    assert L.net2_sha2_ctx_init(1, None) == 0
+    L.SHA256Init(None)
+    assert L.net2_sha2_ctx_update(1, None, buf, 1) == errno.EINVAL
+    assert L.net2_sha2_ctx_init(3, ctx) == 0
+    before = ctx.raw
+    assert L.net2_sha2_ctx_update(3, ctx, None, 0) == 0
+    assert ctx.raw == before
+    assert L.net2_sha2_ctx_transform(2, None, buf) == errno.EINVAL
 
 
 def test_factory_key_rules():
@@ -132,6 +147,15 @@ def test_no_device_fails_loudly():
     with pytest.raises(_lib.Net2Error) as ei:
         h.sha256().run(b"", b"abc")
     assert ei.value.errno == errno.ENODEV
+    # the streaming context: buffering is host bookkeeping, a compression
+    # needs the device (and the context is left as it was)
+    ctx = ctypes.create_string_buffer(208)
+    assert L.net2_sha2_ctx_init(1, ctx) == 0
+    assert L.net2_sha2_ctx_update(1, ctx, buf, 10) == 0
+    before = ctx.raw
+    assert L.net2_sha2_ctx_update(1, ctx, buf, 64) == errno.ENODEV
+    assert ctx.raw == before
+    assert L.net2_sha2_ctx_final(1, buf, ctx) == errno.ENODEV
 
 
 def test_missing_library_fails_loudly():

@@ -1,0 +1,234 @@
+"""The single-message entry points on the GPU: the streaming SHA2_CTX
+interface of src/sha2.c (include/net2/sha2.h), net2_hashctx_hashiov and
+net2_ph_to_iv, all running through the request coalescer
+(ilias_net2_amd/csrc/sha2_coalesce.cpp), alone and from many threads at once.
+
+The streaming calls are compared with the oracle's restatement of the same
+calls (oracle/sha2_oracle.c) context byte for context byte after every call:
+state, bit count and the buffer as src/sha2.c leaves it
+(src/sha2.c:449-563, :738-919).
+"""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+PFX = {1: "SHA256", 2: "SHA384", 3: "SHA512"}
+OPFX = {1: "sha256", 2: "sha384", 3: "sha512"}
+DL = {1: 32, 2: 48, 3: 64}
+BL = {1: 64, 2: 128, 3: 128}
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a GPU (HIP device not visible)")
+    from ilias_net2_amd import _lib
+    assert _lib.device_count() >= 1
+    return _lib.lib()
+
+
+def _ctx():
+    return ctypes.create_string_buffer(208)
+
+
+def _buf(b: bytes):
+    return ctypes.create_string_buffer(b, max(len(b), 1))
+
+
+def test_streaming_matches_oracle_call_by_call(L, oracle_mod):
+    O = oracle_mod.lib()
+    rng = np.random.default_rng(1)
+    for alg in (1, 2, 3):
+        p, op = PFX[alg], OPFX[alg]
+        for n in (0, 1, 55, 56, 63, 64, 65, 111, 112, 119, 120, 127, 128,
+                  129, 1000, 4097):
+            m = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            cuts = sorted(rng.integers(0, n + 1, 5).tolist())
+            chunks = [m[a:b] for a, b in zip([0] + cuts, cuts + [n])]
+            c, oc = _ctx(), _ctx()
+            getattr(L, p + "Init")(c)
+            getattr(O, f"oracle_{op}_init")(oc)
+            assert c.raw == oc.raw
+            for ch in chunks:
+                b = _buf(ch)
+                getattr(L, p + "Update")(c, b, len(ch))
+                getattr(O, f"oracle_{op}_update")(oc, b, len(ch))
+                assert c.raw == oc.raw, (alg, n, len(ch))
+            d, od = ctypes.create_string_buffer(64), ctypes.create_string_buffer(64)
+            getattr(L, p + "Final")(d, c)
+            getattr(O, f"oracle_{op}_final")(od, oc)
+            assert d.raw[:DL[alg]] == od.raw[:DL[alg]] == oracle_mod.digest(alg, m)
+            assert c.raw == oc.raw == b"\0" * 208
+
+
+def test_pad_and_final_null(L, oracle_mod):
+    """Pad alone, and Final(NULL) keeping the padded context for SHA-256 /
+    SHA-512 while SHA-384 zeroes it (src/sha2.c:551-562, :918)."""
+    O = oracle_mod.lib()
+    for alg in (1, 2, 3):
+        p, op = PFX[alg], OPFX[alg]
+        for n in (3, BL[alg] - 9, BL[alg] - 8, BL[alg]):
+            m = _buf(bytes(range(n)))
+            c, oc = _ctx(), _ctx()
+            getattr(L, p + "Init")(c)
+            getattr(O, f"oracle_{op}_init")(oc)
+            getattr(L, p + "Update")(c, m, n)
+            getattr(O, f"oracle_{op}_update")(oc, m, n)
+            getattr(L, p + "Pad")(c)
+            getattr(O, f"oracle_{op}_pad")(oc)
+            assert c.raw == oc.raw, (alg, n)
+            getattr(L, p + "Final")(None, c)
+            getattr(O, f"oracle_{op}_final")(None, oc)
+            assert c.raw == oc.raw, (alg, n)
+            assert (c.raw == b"\0" * 208) == (alg == 2)
+
+
+def test_transform(L, oracle_mod):
+    O = oracle_mod.lib()
+    rng = np.random.default_rng(2)
+    for alg, words, ct in ((1, 8, ctypes.c_uint32), (2, 8, ctypes.c_uint64),
+                           (3, 8, ctypes.c_uint64)):
+        blk = _buf(rng.integers(0, 256, BL[alg], dtype=np.uint8).tobytes())
+        st = (ct * words)(*[int(x) for x in rng.integers(0, 2**31, words)])
+        ost = (ct * words)(*st)
+        getattr(L, PFX[alg] + "Transform")(st, blk)
+        getattr(O, "oracle_sha256_transform" if alg == 1 else
+                "oracle_sha512_transform")(ost, blk)
+        assert list(st) == list(ost)
+        # error form: same result, state unchanged on a bad row
+        st2 = (ct * words)(*[int(x) for x in range(words)])
+        ost2 = (ct * words)(*st2)
+        assert L.net2_sha2_ctx_transform(alg, st2, blk) == 0
+        getattr(O, "oracle_sha256_transform" if alg == 1 else
+                "oracle_sha512_transform")(ost2, blk)
+        assert list(st2) == list(ost2)
+
+
+def test_hashiov_sizes(L, oracle_mod):
+    """Empty, boundary and multi-MiB messages (the staging grows), every row."""
+    from ilias_net2_amd import hash as h
+    rng = np.random.default_rng(3)
+    for n in (0, 1, 55, 56, 64, 111, 112, 128, 1500, 65536, 5 << 20):
+        m = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        for alg in (1, 2, 3):
+            assert h.hashbuf(alg, b"", m) == oracle_mod.digest(alg, m), (alg, n)
+        for alg in (4, 5, 6):
+            key = bytes(range(DL[alg - 3]))
+            assert h.hashbuf(alg, key, m) == oracle_mod.hmac(alg, key, m), (alg, n)
+
+
+def _registry_key(key: bytes, alg: int) -> bytes:
+    """RFC 2104: K' is K (hashed first if longer than the block) zero-padded
+    to the block, so any zero extension of that up to the block gives the
+    same MAC -- here to the registry's key length (= hashlen,
+    hash-openssl.cc:417-429)."""
+    import hashlib
+    h = {4: hashlib.sha256, 5: hashlib.sha384, 6: hashlib.sha512}[alg]
+    blk = 64 if alg == 4 else 128
+    k = h(key).digest() if len(key) > blk else key
+    kl = {4: 32, 5: 48, 6: 64}[alg]
+    assert len(k) <= kl
+    return k + b"\0" * (kl - len(k))
+
+
+def test_rfc4231_on_gpu(L, golden):
+    """RFC 4231 cases 1-7 through the keyed rows of net2_hashctx_hashiov,
+    every key expressed at the registry's key length."""
+    from ilias_net2_amd import hash as h
+    for c in golden["kat"]["rfc4231"]:
+        key, data = bytes.fromhex(c["key"]), bytes.fromhex(c["data"])
+        for alg, name in ((4, "HMAC-SHA256"), (5, "HMAC-SHA384"),
+                          (6, "HMAC-SHA512")):
+            want = c[name]
+            got = h.hashbuf(alg, _registry_key(key, alg), data).hex()
+            assert got[:len(want)] == want, (c["case"], name)
+
+
+def test_many_threads_mixed(L, oracle_mod):
+    """64 threads at once, mixing digests, HMACs, streaming contexts and
+    IV derivations of every row, so batches hold SHA-256 and SHA-512 jobs
+    of all kinds; every result against the oracle."""
+    from ilias_net2_amd import hash as h
+
+    class PH(ctypes.Structure):
+        _fields_ = [("seq", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+    errors = []
+
+    def worker(t):
+        try:
+            rng = np.random.default_rng(100 + t)
+            for j in range(30):
+                kind = (t + j) % 4
+                n = int(rng.integers(0, 2500))
+                m = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+                alg = 1 + int(rng.integers(0, 3))
+                if kind == 0:
+                    if h.hashbuf(alg, b"", m) != oracle_mod.digest(alg, m):
+                        errors.append(("digest", t, j))
+                elif kind == 1:
+                    key = rng.integers(0, 256, DL[alg], dtype=np.uint8).tobytes()
+                    if h.hashbuf(alg + 3, key, m) != oracle_mod.hmac(alg + 3, key, m):
+                        errors.append(("hmac", t, j))
+                elif kind == 2:
+                    c = _ctx()
+                    getattr(L, PFX[alg] + "Init")(c)
+                    for a in range(0, n, 333):
+                        b = _buf(m[a:a + 333])
+                        getattr(L, PFX[alg] + "Update")(c, b, len(m[a:a + 333]))
+                    d = ctypes.create_string_buffer(64)
+                    getattr(L, PFX[alg] + "Final")(d, c)
+                    if d.raw[:DL[alg]] != oracle_mod.digest(alg, m):
+                        errors.append(("ctx", t, j))
+                else:
+                    seq, fl = int(rng.integers(0, 2**32)), int(rng.integers(0, 2**32))
+                    ivlen = int(rng.integers(1, 80))
+                    out = ctypes.create_string_buffer(ivlen)
+                    rc = L.net2_ph_to_iv(ctypes.byref(PH(seq, fl)), ivlen, out)
+                    if rc != 0 or out.raw[:ivlen] != oracle_mod.ph_to_iv(seq, fl, ivlen):
+                        errors.append(("iv", t, j, rc))
+        except Exception as e:  # noqa: BLE001
+            errors.append(("exc", t, repr(e)))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(64)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errors, errors[:5]
+
+
+def test_coalesced_batches_form(L, oracle_mod):
+    """Under concurrency the calls really share launches: 32 threads x 50
+    calls of a 1 KiB SHA-512 finish in far fewer batches than calls (the
+    aggregate rate is well above one call per kernel latency)."""
+    import time
+    from ilias_net2_amd import hash as h
+    m = bytes(range(256)) * 4
+    want = oracle_mod.digest(3, m)
+    h.hashbuf(3, b"", m)
+    t0 = time.perf_counter()
+    for _ in range(50):
+        assert h.hashbuf(3, b"", m) == want
+    single = (time.perf_counter() - t0) / 50
+    bad = []
+
+    def worker():
+        for _ in range(50):
+            if h.hashbuf(3, b"", m) != want:
+                bad.append(1)
+    ths = [threading.Thread(target=worker) for _ in range(32)]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    el = time.perf_counter() - t0
+    assert not bad
+    # 1,600 calls; serialised they would take 1600 * single
+    assert el < 1600 * single / 4, (el, single)
