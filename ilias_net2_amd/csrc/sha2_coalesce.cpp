@@ -30,7 +30,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <memory>
@@ -63,7 +68,7 @@ struct Job {
 	Net2Job desc;		/* offsets relative to the slot's staging */
 	int kind, alg;
 	uint8_t *out;
-	bool done = false;
+	std::atomic<int> done{0};
 	int rc = 0;
 	int hip = 0;		/* HIP error behind rc == EIO */
 };
@@ -73,13 +78,17 @@ struct Slot {
 	hipEvent_t ev = nullptr;
 	uint8_t *h_stage = nullptr, *d_stage = nullptr;
 	size_t cap = 0;
-	uint8_t *h_out = nullptr, *d_out = nullptr;
+	uint8_t *h_out = nullptr;	/* coherent, written by the kernel */
 	size_t cap_jobs = 0;
 	/* the batch being filled or run */
 	std::vector<Job *> jobs;
 	size_t used = 0;
-	int writers = 0;
+	std::atomic<int> writers{0};	/* reservations still being filled */
 	bool full = false;
+	/* completion: every wave of the batch's launches adds 1 here (host
+	 * memory, written by the GPU) once its results are stored */
+	uint32_t *h_done = nullptr;
+	uint32_t done_base = 0;
 	clk::time_point opened;
 
 	void free_stage()
@@ -92,8 +101,7 @@ struct Slot {
 	void free_out()
 	{
 		if (h_out) (void)hipHostFree(h_out);
-		if (d_out && d_out != h_out) (void)hipFree(d_out);
-		h_out = d_out = nullptr;
+		h_out = nullptr;
 		cap_jobs = 0;
 	}
 };
@@ -108,6 +116,21 @@ hipError_t host_alloc(uint8_t **p, size_t bytes, bool zerocopy)
 {
 	return hipHostMalloc((void **)p, bytes, zerocopy ?
 	    (hipHostMallocMapped | hipHostMallocCoherent) : hipHostMallocDefault);
+}
+
+/* Linux futex on a job's completion word: the leader wakes exactly the
+ * callers of its batch (a shared condition variable woke every waiting
+ * thread on every completion, and they queued on one mutex). */
+void futex_wait(std::atomic<int> *w, int val)
+{
+	syscall(SYS_futex, reinterpret_cast<int *>(w), FUTEX_WAIT_PRIVATE, val,
+	    nullptr, nullptr, 0);
+}
+
+void futex_wake(std::atomic<int> *w)
+{
+	syscall(SYS_futex, reinterpret_cast<int *>(w), FUTEX_WAKE_PRIVATE,
+	    INT32_MAX, nullptr, nullptr, 0);
 }
 
 class Coalescer {
@@ -129,7 +152,8 @@ private:
 	int launch_and_wait(Slot &s, int ordinal, int *hip_err);
 
 	std::mutex mu_;
-	std::condition_variable cv_;
+	std::condition_variable slot_cv_;	/* open batch / free slots */
+	std::condition_variable lead_cv_;	/* leaders: inflight, full */
 	Slot slot_[kMaxSlots];
 	const int nslots_;
 	const clk::duration window_;
@@ -251,12 +275,11 @@ int Coalescer::submit(int ordinal, const Request &r, int *hip_err)
 	job.alg = r.alg;
 	job.out = r.out;
 	std::unique_lock<std::mutex> lk(mu_);
-	Slot *sp;
 	int si;
 	for (;;) {
 		if (open_ < 0) {
 			if (free_.empty()) {
-				cv_.wait(lk);
+				slot_cv_.wait(lk);
 				continue;
 			}
 			open_ = free_.back();
@@ -264,7 +287,6 @@ int Coalescer::submit(int ordinal, const Request &r, int *hip_err)
 			Slot &s = slot_[open_];
 			s.jobs.clear();
 			s.used = 0;
-			s.writers = 0;
 			s.full = false;
 			s.opened = clk::now();
 		}
@@ -280,20 +302,21 @@ int Coalescer::submit(int ordinal, const Request &r, int *hip_err)
 		}
 		/* no room: the leader launches it now; join the next batch */
 		s.full = true;
+		lead_cv_.notify_all();
 		const int cur = open_;
-		cv_.notify_all();
-		cv_.wait(lk, [&]() { return open_ != cur; });
+		slot_cv_.wait(lk, [&]() { return open_ != cur; });
 	}
 	si = open_;
-	sp = &slot_[si];
-	Slot &s = *sp;
+	Slot &s = slot_[si];
 	const size_t off = s.used;
 	s.used += need;
 	s.jobs.push_back(&job);
-	s.writers++;
+	s.writers.fetch_add(1, std::memory_order_relaxed);
 	const bool leader = s.jobs.size() == 1;
-	if (!leader && s.used + 2 * 1024 > s.cap)
+	if (!leader && s.used + 2 * 1024 > s.cap) {
 		s.full = true;
+		lead_cv_.notify_all();
+	}
 	lk.unlock();
 
 	/* lay the job out in staging (no lock: the range is ours) */
@@ -316,12 +339,14 @@ int Coalescer::submit(int ordinal, const Request &r, int *hip_err)
 		memcpy(p + body, r.state, blk == 64 ? 32 : 64);
 		job.desc.flags |= NET2_JOB_STATE;
 	}
+	s.writers.fetch_sub(1, std::memory_order_release);
 
-	lk.lock();
-	if (--s.writers == 0)
-		cv_.notify_all();
 	if (!leader) {
-		cv_.wait(lk, [&]() { return job.done; });
+		/* a short spin, then sleep until the leader posts our result */
+		for (int i = 0; i < 256 && !job.done.load(std::memory_order_acquire); i++)
+			__builtin_ia32_pause();
+		while (!job.done.load(std::memory_order_acquire))
+			futex_wait(&job.done, 0);
 		if (job.rc == EIO && hip_err != nullptr)
 			*hip_err = job.hip;
 		return job.rc;
@@ -329,31 +354,40 @@ int Coalescer::submit(int ordinal, const Request &r, int *hip_err)
 
 	/* leader: launch when the device is idle, the batch full, or the
 	 * window over */
-	cv_.wait_until(lk, s.opened + window_, [&]() {
+	lk.lock();
+	lead_cv_.wait_until(lk, s.opened + window_, [&]() {
 		return inflight_ == 0 || s.full;
 	});
-	if (open_ == si)
+	if (open_ == si) {
 		open_ = -1;		/* later callers open the next batch */
-	cv_.wait(lk, [&]() { return s.writers == 0; });
+		slot_cv_.notify_all();
+	}
 	inflight_++;
-	cv_.notify_all();		/* callers waiting for a new open batch */
 	lk.unlock();
+	/* every reservation is in (the batch is closed); wait for the copies */
+	while (s.writers.load(std::memory_order_acquire) != 0)
+		__builtin_ia32_pause();
 
 	int herr = 0;
 	const int rc = launch_and_wait(s, ordinal, &herr);
 	if (rc == EIO && hip_err != nullptr)
 		*hip_err = herr;
-
-	lk.lock();
 	for (Job *jp : s.jobs) {
+		if (jp == &job)
+			continue;
 		jp->rc = rc;
 		jp->hip = herr;
-		jp->done = true;
+		std::atomic<int> *w = &jp->done;
+		w->store(1, std::memory_order_release);
+		futex_wake(w);		/* jp may be gone now; the address is inert */
 	}
+
+	lk.lock();
 	s.jobs.clear();
 	inflight_--;
 	free_.push_back(si);
-	cv_.notify_all();
+	lead_cv_.notify_all();
+	slot_cv_.notify_all();
 	return rc;
 }
 
@@ -406,25 +440,31 @@ int Coalescer::launch_and_wait(Slot &s, int ordinal, int *hip_err)
 	std::vector<Job *> &jobs = s.jobs;
 	const size_t n = jobs.size();
 	size_t hdr_off, n256;
+	uint32_t waves, target;
 	const uint8_t *stage;
-	const Net2Job *descs;
-	uint8_t *out;
+	uint8_t *d_out;
+	uint32_t *d_done;
 
 	CO_TRY(hipSetDevice(ordinal));
 	if (s.stream == nullptr) {
 		CO_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
 		CO_TRY(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+		CO_TRY(hipHostMalloc((void **)&s.h_done, 64,
+		    hipHostMallocMapped | hipHostMallocCoherent));
+		*s.h_done = 0;
+		s.done_base = 0;
 	}
 	if (s.cap_jobs < n) {
+		/* results are written by the kernel straight into coherent
+		 * host memory: no copy back, no wait for one */
 		const size_t want = std::max<size_t>(n + n / 2, 256);
 		s.free_out();
-		CO_TRY(host_alloc(&s.h_out, want * 64, zerocopy_));
-		if (zerocopy_)
-			CO_TRY(hipHostGetDevicePointer((void **)&s.d_out, s.h_out, 0));
-		else
-			CO_TRY(hipMalloc((void **)&s.d_out, want * 64));
+		CO_TRY(hipHostMalloc((void **)&s.h_out, want * 64,
+		    hipHostMallocMapped | hipHostMallocCoherent));
 		s.cap_jobs = want;
 	}
+	CO_TRY(hipHostGetDevicePointer((void **)&d_out, s.h_out, 0));
+	CO_TRY(hipHostGetDevicePointer((void **)&d_done, s.h_done, 0));
 	/* SHA-256 jobs first, then SHA-384/512; longest first within each,
 	 * so a wave's lanes share their trip count as far as possible */
 	std::sort(jobs.begin(), jobs.end(), [](const Job *a, const Job *b) {
@@ -440,38 +480,46 @@ int Coalescer::launch_and_wait(Slot &s, int ordinal, int *hip_err)
 		    sizeof(Net2Job));
 		n256 += jobs[k]->alg == 1;
 	}
-	if (zerocopy_) {
-		stage = s.d_stage;
-	} else {
+	if (!zerocopy_)
 		CO_TRY(hipMemcpyAsync(s.d_stage, s.h_stage,
 		    hdr_off + n * sizeof(Net2Job), hipMemcpyHostToDevice,
 		    s.stream));
-		stage = s.d_stage;
-	}
-	descs = reinterpret_cast<const Net2Job *>(stage + hdr_off);
-	out = s.d_out;
-	CO_TRY(net2_launch_jobs(stage, descs, (uint32_t)n256,
-	    (uint32_t)(n - n256), out, s.stream));
-	if (!zerocopy_)
-		CO_TRY(hipMemcpyAsync(s.h_out, s.d_out, n * 64,
-		    hipMemcpyDeviceToHost, s.stream));
+	stage = s.d_stage;
+	waves = (uint32_t)((n256 + 63) / 64 + (n - n256 + 63) / 64);
+	target = s.done_base + waves;
+	CO_TRY(net2_launch_jobs(stage,
+	    reinterpret_cast<const Net2Job *>(stage + hdr_off), (uint32_t)n256,
+	    (uint32_t)(n - n256), d_out, d_done, s.stream));
 	CO_TRY(hipEventRecord(s.ev, s.stream));
 	{
-		/* a small batch finishes in tens of microseconds: spin on the
-		 * event (a blocking wait adds a wake-up), then block */
+		/*
+		 * Done when every wave has counted itself in (each stores its
+		 * results first, then adds 1 with system-scope release order).
+		 * A small batch takes tens of microseconds: poll the host word
+		 * (no runtime call, no end-of-kernel latency); after a few
+		 * milliseconds fall back to the event, which also reports a
+		 * kernel that failed.
+		 */
 		const clk::time_point t0 = clk::now();
-		for (;;) {
-			e = hipEventQuery(s.ev);
-			if (e != hipErrorNotReady)
-				break;
-			if (clk::now() - t0 > std::chrono::milliseconds(2)) {
-				e = hipEventSynchronize(s.ev);
+		bool ok = false;
+		for (unsigned i = 1;; i++) {
+			if (__atomic_load_n(s.h_done, __ATOMIC_ACQUIRE) == target) {
+				ok = true;
 				break;
 			}
+			if ((i & 255) == 0 &&
+			    clk::now() - t0 > std::chrono::milliseconds(5))
+				break;
 			__builtin_ia32_pause();
 		}
-		if (e != hipSuccess)
-			goto fail;
+		if (!ok) {
+			CO_TRY(hipEventSynchronize(s.ev));
+			if (__atomic_load_n(s.h_done, __ATOMIC_ACQUIRE) != target) {
+				e = hipErrorLaunchFailure;
+				goto fail;
+			}
+		}
+		s.done_base = target;
 	}
 	for (size_t k = 0; k < n; k++)
 		deliver(*jobs[k], s.h_out + 64 * k);
@@ -480,6 +528,10 @@ fail:
 	if (hip_err != nullptr)
 		*hip_err = (int)e;
 	(void)hipGetLastError();
+	/* the counter may be anywhere now: resynchronise it */
+	if (s.stream != nullptr && hipStreamSynchronize(s.stream) == hipSuccess &&
+	    s.h_done != nullptr)
+		s.done_base = __atomic_load_n(s.h_done, __ATOMIC_ACQUIRE);
 	return e == hipErrorOutOfMemory ? ENOMEM : EIO;
 #undef CO_TRY
 }

@@ -970,7 +970,8 @@ __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ b
  */
 template <class H>
 __global__ __launch_bounds__(64) void job_kernel(const uint8_t *__restrict__ stage,
-    const Net2Job *__restrict__ jobs, uint32_t n, uint8_t *__restrict__ out)
+    const Net2Job *__restrict__ jobs, uint32_t n, uint8_t *__restrict__ out,
+    uint32_t *done)
 {
 	constexpr int NW32 = H::NW32;
 	typedef typename H::word W;
@@ -1018,6 +1019,12 @@ __global__ __launch_bounds__(64) void job_kernel(const uint8_t *__restrict__ sta
 #pragma unroll
 	for (int i = 0; i < 8; i++)
 		o[i] = st[i];
+	/* count the wave in once all of its lanes' results are visible to the
+	 * host (the workgroup is one wave; lane 0 is always live) */
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+	if (threadIdx.x == 0)
+		__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELEASE,
+		    __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 /* ---- packet-header IV derivation (types/packet.n2t:100-158) ---------------- */
@@ -1523,15 +1530,16 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 	return hipGetLastError();
 }
 hipError_t net2_launch_jobs(const uint8_t *stage, const Net2Job *jobs,
-    uint32_t n256, uint32_t n512, uint8_t *out, hipStream_t s)
+    uint32_t n256, uint32_t n512, uint8_t *out, uint32_t *done,
+    hipStream_t s)
 {
 	/* 64-lane workgroups: a few jobs spread over as many CUs as waves */
 	if (n256 > 0)
 		job_kernel<Sha256><<<(n256 + 63) / 64, 64, 0, s>>>(stage, jobs,
-		    n256, out);
+		    n256, out, done);
 	if (n512 > 0)
 		job_kernel<Sha512><<<(n512 + 63) / 64, 64, 0, s>>>(stage,
-		    jobs + n256, n512, out + 64 * (size_t)n256);
+		    jobs + n256, n512, out + 64 * (size_t)n256, done);
 	return hipGetLastError();
 }
 

@@ -71,7 +71,8 @@ struct Net2Job {
 };
 /* jobs [0, n256) are SHA-256, [n256, n256 + n512) SHA-384/512. */
 hipError_t net2_launch_jobs(const uint8_t *stage, const Net2Job *jobs,
-    uint32_t n256, uint32_t n512, uint8_t *out, hipStream_t s);
+    uint32_t n256, uint32_t n512, uint8_t *out, uint32_t *done,
+    hipStream_t s);
 
 /* Packet-header IVs (ivlen <= 64): out = n x ivlen bytes. */
 hipError_t net2_launch_ph_iv(const uint32_t *seq, const uint32_t *flags,
