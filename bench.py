@@ -118,50 +118,112 @@ def _smt_active():
         return None
 
 
+def _cpu_topology():
+    """Physical cores and sockets from /proc/cpuinfo, cgroup CPU quota."""
+    phys, cores_per = set(), None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("physical id"):
+                    phys.add(line.split(":")[1].strip())
+                elif line.startswith("cpu cores") and cores_per is None:
+                    cores_per = int(line.split(":")[1])
+    except OSError:
+        pass
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                quota = f.read().strip()
+            break
+        except OSError:
+            continue
+    return {"physical_cores": (cores_per or 0) * max(len(phys), 1) or None,
+            "sockets": len(phys) or None, "cgroup_cpu_quota": quota}
+
+
+def _time_oracle(run, threads, reps=3):
+    run(threads)  # warm-up (page faults, thread start)
+    best = float("inf")
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        run(threads)
+        best = min(best, time.perf_counter() - t0)
+    return best
+
+
 def cpu_baseline(cfg):
-    """Oracle (clean-room C restatement of src/sha2.c, -O3) on host cores."""
-    import numpy as np
+    """Oracle (clean-room C restatement of src/sha2.c, -O3) on the host
+    cores of the GPU box: every usable host CPU (the headline value), the
+    per-GPU share of 16 threads, and one thread."""
     from oracle import oracle
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import synth
-    threads = min(16, len(os.sched_getaffinity(0)))
+    affinity = len(os.sched_getaffinity(0))
+    share = min(16, affinity)
+    allc = min(256, affinity)          # oracle_sha2_batch caps at 256 threads
     alg = cfg["alg"]
     n = cfg["n"]
     if cfg["kind"] == "fixed":
         data = synth.fixed_batch(2, n, cfg["length"])
-        run = lambda t: oracle.batch(alg, data, stride=cfg["length"],  # noqa: E731
-                                     length=cfg["length"], n=n, nthreads=t)
+        run = lambda t, m=n: oracle.batch(alg, data, stride=cfg["length"],  # noqa: E731
+                                          length=cfg["length"], n=m, nthreads=t)
     else:
         lens = synth.mixed_lengths(3, n)
         data, offs = synth.packed(4, lens)
-        run = lambda t: oracle.batch(alg, data, offsets=offs, lens=lens,  # noqa: E731
-                                     nthreads=t)
-    run(threads)  # warm-up (page faults, thread start)
-    best = float("inf")
-    for _ in range(3):
-        t0 = time.perf_counter()
-        run(threads)
-        best = min(best, time.perf_counter() - t0)
-    # SURVEY 8(d): also one thread, on the first n/16 packets (same shape)
+        run = lambda t, m=n: oracle.batch(alg, data, offsets=offs[:m],  # noqa: E731
+                                          lens=lens[:m], nthreads=t)
+    t_share = _time_oracle(run, share)
+    t_all = _time_oracle(run, allc, reps=5)
+    # one thread, on the first n/16 packets (same shape)
     n1 = max(1, n // 16)
-    if cfg["kind"] == "fixed":
-        one = lambda: oracle.batch(alg, data, stride=cfg["length"],  # noqa: E731
-                                   length=cfg["length"], n=n1, nthreads=1)
-    else:
-        one = lambda: oracle.batch(alg, data, offsets=offs[:n1], lens=lens[:n1],  # noqa: E731
-                                   nthreads=1)
     t0 = time.perf_counter()
-    one()
+    run(1, n1)
     single = n1 / (time.perf_counter() - t0)
-    return {"value": n / best, "unit": "digests/s", "cores": threads,
-            "single_thread_value": single, "cpu_model": _cpu_model(),
-            "host_cpus": os.cpu_count(),
-            "affinity_cpus": len(os.sched_getaffinity(0)),
-            "smt_active": _smt_active(),
+    what = cfg["workload"].split(" packets")[0]
+    return {"value": n / t_all, "unit": "digests/s", "cores": allc,
             "kind": "port",
-            "sample": (f"the full {cfg['workload'].split(' packets')[0]} packet batch from host memory, "
-                       f"oracle/sha2_oracle.c (-O3, rolled transform like src/sha2.c:374-445) "
-                       f"on {threads} pthreads, best of 3 after a warm-up")}
+            "sample": (f"the full {what} packet batch from host memory, "
+                       f"oracle/sha2_oracle.c (-O3, rolled transform like "
+                       f"src/sha2.c:374-445) on {allc} pthreads = every CPU "
+                       f"the process may use, best of 5 after a warm-up"),
+            "per_gpu_share": {"value": n / t_share, "threads": share,
+                              "note": "16 host threads = one GPU's share of the node's CPUs, best of 3"},
+            "single_thread_value": single,
+            "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
+            "affinity_cpus": affinity, "smt_active": _smt_active(),
+            **_cpu_topology()}
+
+
+def gpu_info(dev):
+    """Name, host and shader clock of the GPU (the box-to-box spread of the
+    pool is larger than run-to-run noise)."""
+    import socket
+    import torch
+    p = torch.cuda.get_device_properties(dev)
+    bus = "%04x:%02x:%02x.0" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+    return {"name": p.name, "arch": p.gcnArchName, "cus": p.multi_processor_count,
+            "pci": bus, "host": socket.gethostname(),
+            "sclk_mhz": read_sclk(bus)}
+
+
+def read_sclk(bus):
+    """(max, current) shader clock in MHz from the amdgpu DPM table."""
+    try:
+        with open(f"/sys/bus/pci/devices/{bus}/pp_dpm_sclk") as f:
+            rows = f.read().split("\n")
+    except OSError:
+        return None
+    mhz, cur = [], None
+    for r in rows:
+        parts = r.replace(":", " ").split()
+        for tok in parts:
+            if tok.lower().endswith("mhz"):
+                v = int(tok[:-3])
+                mhz.append(v)
+                if "*" in r:
+                    cur = v
+    return {"max": max(mhz) if mhz else None, "current": cur}
 
 
 def load_pmc(config_name):
@@ -184,6 +246,170 @@ def load_isa_mix(config_name):
         return json.load(f)["configs"].get(config_name)
 
 
+def device_step(name, inp, out, ws_buf, stream, unbinned=False):
+    """One step of a device-resident config: one pass of the hot path over
+    the whole batch (one launch, plus the binning launches of the variable
+    layout)."""
+    from ilias_net2_amd import batch, _lib
+    cfg = CONFIGS[name]
+    L = _lib.lib()
+    n, alg = inp["n"], cfg["alg"]
+    kbuf = HMAC_KEY[:DLEN[alg]] if alg >= 4 else b""
+    if cfg["kind"] == "dgram_verify":
+        return lambda: _lib.check(L.net2_hmac_verify_dev(
+            alg, kbuf, len(kbuf), inp["data"].data_ptr(),
+            inp["offs"].data_ptr(), inp["lens"].data_ptr(), n,
+            out.data_ptr(), ws_buf.data_ptr(), ws_buf.numel() * 4,
+            stream.cuda_stream))
+    if cfg["kind"] == "ph_iv":
+        return lambda: _lib.check(L.net2_ph_to_iv_dev(
+            inp["seq"].data_ptr(), inp["flags"].data_ptr(), n, cfg["length"],
+            out.data_ptr(), stream.cuda_stream))
+    if alg >= 4:
+        mixed = cfg["kind"] == "mixed"
+        return lambda: _lib.check(L.net2_hmac_dev(
+            alg, kbuf, len(kbuf), inp["data"].data_ptr(),
+            inp["offs"].data_ptr() if mixed else None,
+            inp["lens"].data_ptr() if mixed else None,
+            cfg["length"] or 0, cfg["length"] or 0, n, out.data_ptr(),
+            ws_buf.data_ptr() if mixed and not unbinned else None,
+            ws_buf.numel() * 4 if mixed else 0, stream.cuda_stream))
+    if cfg["kind"] == "fixed":
+        return lambda: batch.digest_fixed(alg, inp["data"], cfg["length"],
+                                          cfg["length"], n, out=out,
+                                          stream=stream)
+    return lambda: batch.digest_var(alg, inp["data"], inp["offs"], inp["lens"],
+                                    out=out, workspace=ws_buf,
+                                    binned=not unbinned, stream=stream)
+
+
+def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
+                       dist_backend="nccl", unbinned=False, clock_probe=None):
+    """Untimed clock ramp and warmup, then exactly `steps` steps between
+    barriers + synchronize; the dominant kernel's duration from HIP events
+    on the launch stream.  Returns the measurements (max over ranks)."""
+    import torch
+    import torch.distributed as dist
+    from ilias_net2_amd import batch
+    cfg = CONFIGS[name]
+    inp = make_inputs(cfg, dev, seed=2 + rank)
+    n, alg = inp["n"], cfg["alg"]
+    dlen = cfg["length"] if cfg["kind"] == "ph_iv" else \
+        1 if cfg["kind"] == "dgram_verify" else DLEN[alg]
+    out = torch.empty((n, dlen), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    ws_buf = batch.var_workspace(n, dev) if cfg["kind"] in ("mixed", "dgram_verify") else None
+    if cfg["kind"] == "dgram_verify":
+        # sign once (untimed) so every datagram verifies
+        batch.hmac_sign_dev(alg, HMAC_KEY[:DLEN[alg]], inp["data"], inp["offs"],
+                            inp["lens"], workspace=ws_buf)
+    step = device_step(name, inp, out, ws_buf, stream, unbinned)
+
+    # Clock ramp: repeat the step (untimed) for prewarm_ms of wall time.
+    t_pw = time.perf_counter()
+    while (time.perf_counter() - t_pw) * 1e3 < prewarm_ms:
+        step()
+        torch.cuda.synchronize(dev)
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    # HIP events on the stream the kernels are launched on.
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        step()
+        b.record(stream)
+    clk = clock_probe() if clock_probe else None  # while the steps run
+    torch.cuda.synchronize(dev)
+    if ws > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    launch_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+
+    if ws > 1:
+        t = torch.tensor([elapsed, launch_ms], dtype=torch.float64,
+                         device=dev if dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, launch_ms = float(t[0]), float(t[1])
+    # algorithmic bytes: payload read + digests written (+ 12 B/packet of
+    # offsets and lengths for the variable layout), per launch
+    per_launch = inp["payload"] + n * dlen + \
+        (12 * n if cfg["kind"] in ("mixed", "dgram_verify") else 0)
+    res = {"n": n, "dlen": dlen, "payload": inp["payload"], "elapsed": elapsed,
+           "ms_per_step": elapsed * 1e3 / steps, "launch_ms": launch_ms,
+           "per_launch_bytes": per_launch, "sclk_during_mhz": clk}
+    del inp, out, ws_buf
+    torch.cuda.empty_cache()
+    return res
+
+
+def rooflines(name, launch_ms, per_launch):
+    """HBM roofline of the dominant kernel (algorithmic bytes over the
+    event-timed launch, PMC traffic from profiles/pmc_<config>.json) and the
+    VALU issue figures that bind these kernels."""
+    achieved = per_launch / (launch_ms / 1e3) / 1e9
+    pmc = load_pmc(name)
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+            "kernel_ms": round(launch_ms, 4),
+            "algorithmic_bytes_per_launch": per_launch}
+    if pmc and pmc.get("hbm_bytes_per_launch"):
+        roof["traffic_over_algorithmic"] = round(pmc["hbm_bytes_per_launch"] / per_launch, 3)
+    valu = None
+    if pmc and pmc.get("valu_wave_instr_per_launch"):
+        instr = pmc["valu_wave_instr_per_launch"]
+        rate = instr / (launch_ms / 1e3)
+        clk = pmc.get("clock_ghz_under_pmc") or 2.4
+        valu = {"bound": "valu", "achieved": round(rate / 1e12, 4),
+                "peak": round(VALU_PEAK_WAVE_INSTR / 1e12, 4),
+                "unit": "T wave64-VALU-instr/s",
+                "frac": round(rate / VALU_PEAK_WAVE_INSTR, 4),
+                # SIMD cycles between VALU issues, averaged over the launch:
+                # 2.0 = the nominal SIMD-32 rate, reached only by full-rate
+                # ops in a pure stream; v_alignbit/v_add3/v_perm are
+                # half-rate (4.2), and a stream mixing the two classes issues
+                # every instruction at ~4 (DESIGN.md 5.3)
+                "simd_cycles_per_valu_instr": round(clk * 1e9 * (launch_ms / 1e3) * 1024 / instr, 3),
+                "clock_ghz": round(clk, 3),
+                "instr_per_launch": instr,
+                "source": "rocprofv3 SQ_INSTS_VALU / GRBM_GUI_ACTIVE, profiles/pmc_%s.json" % name}
+        mix = load_isa_mix(name)
+        if mix and mix.get("mean_issue_cycles_per_valu_instr"):
+            # Issue floor: every VALU instruction of the launch priced at the
+            # measured issue cost of a mixed half/full-rate stream
+            # (tools/isa_mix.py, probe cycles at 2.4 GHz like the probe).
+            m = mix["mean_issue_cycles_per_valu_instr"]
+            floor_ms = instr / 1024 * m / 2.4e9 * 1e3
+            valu["issue_floor"] = {
+                "mean_cycles_per_valu_instr": m,
+                "floor_ms": round(floor_ms, 4),
+                "frac": round(floor_ms / launch_ms, 4),
+                "source": "profiles/isa_mix.json (mixed-stream model) x profiles/round1/valu_bank_seq_probe.json (cost)"}
+    return roof, valu
+
+
+def metric_of(name):
+    cfg = CONFIGS[name]
+    alg = cfg["alg"]
+    if name == "c2":
+        return METRIC
+    return (("SHA-256 IVs/s, " if cfg["kind"] == "ph_iv" else
+             f"{ALG_NAMES[alg]} datagrams verified/s, " if cfg["kind"] == "dgram_verify" else
+             f"{ALG_NAMES[alg]} digests/s, ") + cfg["workload"])
+
+
+def unit_of(name):
+    kind = CONFIGS[name]["kind"]
+    return "datagrams/s" if kind == "dgram_verify" else "IVs/s" if kind == "ph_iv" else "digests/s"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -193,8 +419,11 @@ def main():
                     help="untimed launches before the warmup steps so the GPU "
                          "reaches its steady-state clock (a cold MI355X runs "
                          "the first ~50 launches ~15%% slower)")
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS) + ["e2e"])
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS) + ["e2e", "c1"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="c2 at N=1: skip the extra BASELINE configs (C1, C3, C4, "
+                         "end to end) that otherwise ride in the same line")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--unbinned", action="store_true",
                     help="c3: hash in submission order (ablation)")
@@ -202,7 +431,7 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from ilias_net2_amd import batch, _lib
+    from ilias_net2_amd import _lib
 
     ws, rank, local = dist_env()
     # One process per GPU.  --dist-backend gloo with more ranks than GPUs
@@ -221,165 +450,79 @@ def main():
 
     if args.config == "e2e":
         return run_e2e(args, ws, rank, dev)
+    if args.config == "c1":
+        print(json.dumps(run_c1()), flush=True)
+        return None
 
-    cfg = CONFIGS[args.config]
-    inp = make_inputs(cfg, dev, seed=2 + rank)
-    n, alg = inp["n"], cfg["alg"]
-    dlen = cfg["length"] if cfg["kind"] == "ph_iv" else \
-        1 if cfg["kind"] == "dgram_verify" else DLEN[alg]
-    out = torch.empty((n, dlen), dtype=torch.uint8, device=dev)
-    ws_buf = batch.var_workspace(n, dev) if cfg["kind"] in ("mixed", "dgram_verify") else None
-    kbuf = HMAC_KEY[:DLEN[alg]] if alg >= 4 else b""
-    if cfg["kind"] == "dgram_verify":
-        # sign once (untimed) so every datagram verifies
-        batch.hmac_sign_dev(alg, kbuf, inp["data"], inp["offs"], inp["lens"])
-    stream = torch.cuda.current_stream(dev)
-    L = _lib.lib()
-
-    def step():
-        if cfg["kind"] == "dgram_verify":
-            _lib.check(L.net2_hmac_verify_dev(
-                alg, kbuf, len(kbuf), inp["data"].data_ptr(),
-                inp["offs"].data_ptr(), inp["lens"].data_ptr(), n,
-                out.data_ptr(), ws_buf.data_ptr(), ws_buf.numel() * 4,
-                stream.cuda_stream))
-        elif cfg["kind"] == "ph_iv":
-            _lib.check(L.net2_ph_to_iv_dev(inp["seq"].data_ptr(), inp["flags"].data_ptr(),
-                                           n, cfg["length"], out.data_ptr(),
-                                           stream.cuda_stream))
-        elif alg >= 4:
-            mixed = cfg["kind"] == "mixed"
-            _lib.check(L.net2_hmac_dev(
-                alg, kbuf, len(kbuf), inp["data"].data_ptr(),
-                inp["offs"].data_ptr() if mixed else None,
-                inp["lens"].data_ptr() if mixed else None,
-                cfg["length"] or 0, cfg["length"] or 0, n, out.data_ptr(),
-                ws_buf.data_ptr() if mixed and not args.unbinned else None,
-                ws_buf.numel() * 4 if mixed else 0, stream.cuda_stream))
-        elif cfg["kind"] == "fixed":
-            batch.digest_fixed(alg, inp["data"], cfg["length"], cfg["length"],
-                               n, out=out, stream=stream)
-        else:
-            batch.digest_var(alg, inp["data"], inp["offs"], inp["lens"],
-                             out=out, workspace=ws_buf,
-                             binned=not args.unbinned, stream=stream)
-
-    # Clock ramp: repeat the step (untimed) for --prewarm-ms of wall time.
-    t_pw = time.perf_counter()
-    while (time.perf_counter() - t_pw) * 1e3 < args.prewarm_ms:
-        step()
-        torch.cuda.synchronize(dev)
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-
-    # HIP events on the stream the kernels are launched on.
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    if ws > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for a, b in ev:
-        a.record(stream)
-        step()
-        b.record(stream)
-    torch.cuda.synchronize(dev)
-    if ws > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    launch_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-
-    if ws > 1:
-        t = torch.tensor([elapsed, launch_ms], dtype=torch.float64,
-                         device=dev if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, launch_ms = float(t[0]), float(t[1])
-
-    ms_per_step = elapsed * 1e3 / args.steps
-    total_digests = n * ws
-    value = total_digests / (ms_per_step / 1e3)
-
-    # Roofline of the dominant kernel: algorithmic bytes = payload read +
-    # digests written (+ 12 B/packet offsets+lens for the mixed layout),
-    # per launch, over the event-timed launch duration.
-    per_launch = inp["payload"] + n * dlen + (12 * n if cfg["kind"] in ("mixed", "dgram_verify") else 0)
-    achieved = per_launch / (launch_ms / 1e3) / 1e9
-    pmc = load_pmc(args.config)
-    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
-            "kernel_ms": round(launch_ms, 4),
-            "algorithmic_bytes_per_launch": per_launch}
-    valu = None
-    if pmc and pmc.get("valu_wave_instr_per_launch"):
-        instr = pmc["valu_wave_instr_per_launch"]
-        rate = instr / (launch_ms / 1e3)
-        clk = pmc.get("clock_ghz_under_pmc") or 2.4
-        valu = {"bound": "valu", "achieved": round(rate / 1e12, 4),
-                "peak": round(VALU_PEAK_WAVE_INSTR / 1e12, 4),
-                "unit": "T wave64-VALU-instr/s",
-                "frac": round(rate / VALU_PEAK_WAVE_INSTR, 4),
-                # SIMD cycles between VALU issues, averaged over the launch:
-                # 2.0 = the nominal SIMD-32 rate, reached only by full-rate
-                # ops in a pure stream; v_alignbit/v_add3/v_perm are
-                # half-rate (4.2), and a stream mixing the two classes issues
-                # every instruction at ~4
-                "simd_cycles_per_valu_instr": round(clk * 1e9 * (launch_ms / 1e3) * 1024 / instr, 3),
-                "clock_ghz": round(clk, 3),
-                "instr_per_launch": instr,
-                "source": "rocprofv3 SQ_INSTS_VALU / GRBM_GUI_ACTIVE, profiles/pmc_%s.json" % args.config}
-        mix = load_isa_mix(args.config)
-        if mix and mix.get("mean_issue_cycles_per_valu_instr"):
-            # Issue floor: every VALU instruction of the launch priced at the
-            # measured issue cost of a mixed half/full-rate stream
-            # (tools/isa_mix.py, probe cycles at 2.4 GHz like the probe).
-            m = mix["mean_issue_cycles_per_valu_instr"]
-            floor_ms = instr / 1024 * m / 2.4e9 * 1e3
-            valu["issue_floor"] = {
-                "mean_cycles_per_valu_instr": m,
-                "floor_ms": round(floor_ms, 4),
-                "frac": round(floor_ms / launch_ms, 4),
-                "source": "profiles/isa_mix.json (mixed-stream model) x profiles/round1/valu_bank_seq_probe.json (cost)"}
-
+    gpu = gpu_info(dev)
+    probe = lambda: (read_sclk(gpu["pci"]) or {}).get("current")  # noqa: E731
+    name = args.config
+    cfg = CONFIGS[name]
+    r = time_device_config(name, dev, args.steps, args.warmup, args.prewarm_ms,
+                           ws, rank, args.dist_backend, args.unbinned, probe)
+    value = r["n"] * ws / (r["ms_per_step"] / 1e3)
+    roof, valu = rooflines(name, r["launch_ms"], r["per_launch_bytes"])
+    alg = cfg["alg"]
     line = {
-        "metric": METRIC if args.config == "c2" else
-        ("SHA-256 IVs/s, " if cfg["kind"] == "ph_iv" else
-         f"{ALG_NAMES[alg]} datagrams verified/s, " if cfg["kind"] == "dgram_verify" else
-         f"{ALG_NAMES[alg]} digests/s, ") + cfg["workload"],
+        "metric": metric_of(name),
         "value": round(value, 1),
-        "unit": "datagrams/s" if cfg["kind"] == "dgram_verify" else "IVs/s" if cfg["kind"] == "ph_iv" else "digests/s",
+        "unit": unit_of(name),
         "n_gpus": ws,
         "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        "ms_per_step": round(r["ms_per_step"], 4), "higher_is_better": True,
         "prewarm_ms": args.prewarm_ms,
         "scaling": "weak", "vs_baseline": None, "dtype": "u64" if alg in (2, 3, 5, 6) else "u32",
         "data": "synthetic: uniform random bytes (torch.randint, seed 2+rank), resident in HBM before timing",
         "config": {"workload": cfg["workload"] + (" [unbinned]" if args.unbinned else ""),
-                   "packets_per_gpu": n,
+                   "packets_per_gpu": r["n"],
                    "alg": ALG_NAMES[alg].replace("-", "") if alg <= 3 else ALG_NAMES[alg],
-                   "payload_bytes_per_gpu": inp["payload"],
+                   "payload_bytes_per_gpu": r["payload"],
                    "parallelism": f"{ws} independent shards, no collective"},
         "roofline": roof,
     }
     if valu:
         line["roofline_valu"] = valu
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline and args.config in ("c2", "c3", "c4"):
+    gpu["sclk_mhz_during_timed_steps"] = r["sclk_during_mhz"]
+    line["gpu"] = gpu
+    if ws == 1 and name == "c2" and not args.no_extras:
+        line["extra_configs"] = extra_configs(args, dev, probe)
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline and name in ("c2", "c3", "c4"):
         line["cpu_baseline"] = cpu_baseline(cfg)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if ws > 1:
         dist.destroy_process_group()
+    return None
 
 
-def run_e2e(args, ws, rank, dev):
-    """Config 5 shape: host memory -> pinned H2D -> kernel -> D2H -> host,
-    through net2_sha2_batch on this rank's device (PCIe-inclusive rate)."""
-    import numpy as np
+def extra_configs(args, dev, probe):
+    """The other BASELINE.json configs, timed in the same invocation on the
+    same GPU: C3 (mixed lengths, binned) and C4 (SHA-512) device-resident
+    with their rooflines; the end-to-end host-memory rate per GPU (C5's
+    per-GPU shape); C1 (4096 x 1 KiB signed payloads)."""
+    out = {}
+    for name in ("c3", "c4"):
+        r = time_device_config(name, dev, args.steps, min(args.warmup, 10),
+                               200.0, clock_probe=probe)
+        roof, valu = rooflines(name, r["launch_ms"], r["per_launch_bytes"])
+        out[name] = {"metric": metric_of(name), "value": round(r["n"] / (r["ms_per_step"] / 1e3), 1),
+                     "unit": unit_of(name), "steps": args.steps,
+                     "ms_per_step": round(r["ms_per_step"], 4),
+                     "workload": CONFIGS[name]["workload"],
+                     "sclk_mhz_during_timed_steps": r["sclk_during_mhz"],
+                     "roofline": roof}
+        if valu:
+            out[name]["roofline_valu"] = valu
+    out["e2e"] = e2e_rate(steps=10, warmup=3)
+    out["c1"] = run_c1()
+    return out
+
+
+def e2e_rate(steps, warmup, n=1 << 20, length=1024):
+    """C5's per-GPU shape: 1 M x 1 KiB from pinned host memory -> this GPU ->
+    digests back to pinned host memory, through net2_sha2_batch."""
     import torch
-    import torch.distributed as dist
     from ilias_net2_amd import _lib
-    n, length = 1 << 20, 1024
     host = torch.randint(0, 256, (n * length,), dtype=torch.uint8).pin_memory()
     outp = torch.empty((n, 32), dtype=torch.uint8).pin_memory()
     L = _lib.lib()
@@ -387,34 +530,56 @@ def run_e2e(args, ws, rank, dev):
     def step():
         _lib.check(L.net2_sha2_batch(1, host.data_ptr(), None, None, length,
                                      length, n, outp.data_ptr(), 1))
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    ms = (time.perf_counter() - t0) * 1e3 / steps
+    del host, outp
+    return {"metric": "SHA-256 digests/s, 1 KiB packets from pinned host memory, "
+                      "end to end (H2D + kernel + D2H), one GPU",
+            "value": round(n / (ms / 1e3), 1), "unit": "digests/s", "steps": steps,
+            "ms_per_step": round(ms, 3),
+            "workload": "1M x 1 KiB per GPU, host -> GPU -> host via net2_sha2_batch (BASELINE configs[4] per-GPU shape)",
+            "h2d_GBps": round(n * length / (ms / 1e3) / 1e9, 2)}
+
+
+def run_c1():
+    """BASELINE configs[0] shape: 4096 x 1 KiB payloads through the signed-
+    payload flow with test/sign.c's P-521 key (tools/bench_sign.py): GPU
+    digests from host memory, the oracle's digests on one core (the
+    reference's per-payload loop), and the batched signature create /
+    validate (ECDSA on host threads)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_sign
+    return bench_sign.measure()
+
+
+def run_e2e(args, ws, rank, dev):
+    """Config 5 shape: host memory -> pinned H2D -> kernel -> D2H -> host,
+    through net2_sha2_batch on this rank's device (PCIe-inclusive rate)."""
+    import torch
+    import torch.distributed as dist
     if ws > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    if ws > 1:
-        dist.barrier()
+    r = e2e_rate(args.steps, args.warmup)
     el = time.perf_counter() - t0
     if ws > 1:
-        t = torch.tensor([el], dtype=torch.float64,
+        t = torch.tensor([r["ms_per_step"]], dtype=torch.float64,
                          device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t[0])
-    ms = el * 1e3 / args.steps
+        r["ms_per_step"] = float(t[0])
+        r["value"] = round((1 << 20) * ws / (r["ms_per_step"] / 1e3), 1)
+    r.update({"n_gpus": ws, "warmup": args.warmup, "higher_is_better": True,
+              "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+              "data": "synthetic random bytes in pinned host memory",
+              "wall_s": round(el, 3)})
     if rank == 0:
-        print(json.dumps({
-            "metric": "SHA-256 digests/s, 1 KiB packets from pinned host memory, end to end (H2D + kernel + D2H)",
-            "value": round(n * ws / (ms / 1e3), 1), "unit": "digests/s", "n_gpus": ws,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "u32", "data": "synthetic random bytes in pinned host memory",
-            "config": {"workload": "1M x 1 KiB per GPU, host -> GPU -> host via net2_sha2_batch",
-                       "h2d_GBps": round(n * length / (ms / 1e3) / 1e9, 2)}}), flush=True)
+        print(json.dumps(r), flush=True)
     if ws > 1:
         dist.destroy_process_group()
-    del np
 
 
 if __name__ == "__main__":

@@ -27,7 +27,21 @@ class Sig(ctypes.Structure):
                 ("data", ctypes.c_void_p), ("datalen", ctypes.c_size_t)]
 
 
-def main():
+def measure():
+    """All stages in one dict (bench.py's extra_configs.c1)."""
+    res = stages()
+    out = {"metric": "signed payloads/s, 4096 x 1 KiB (BASELINE configs[0] shape), "
+                     "hash-then-sign / validate with the P-521 key of test/sign.c",
+           "workload": "4096 x 1 KiB payloads, SHA-512 sighash (the negotiated default) "
+                       "and SHA-256, ECDSA-P521 on host threads",
+           "stages": {}}
+    for r in res:
+        out["stages"][r["key"]] = {k: (round(v, 3) if isinstance(v, float) else v)
+                                   for k, v in r.items() if k != "key"}
+    return out
+
+
+def stages():
     import ilias_net2_amd._lib as L
     from oracle import oracle
     import synth
@@ -64,11 +78,13 @@ def main():
         dig = np.empty((n, 64 if alg == 3 else 32), dtype=np.uint8)
         t = timeit(lambda: L.check(L.lib().net2_sha2_batch(
             alg, ptr(data), ptr(offs), ptr(lens), 0, 0, n, ptr(dig), 1)))
-        res.append({"stage": f"GPU digest {name} (net2_sha2_batch, host mem, 1 GPU)",
+        res.append({"key": f"gpu_digest_{name.lower()}",
+                     "stage": f"GPU digest {name} (net2_sha2_batch, host mem, 1 GPU)",
                     "payloads_per_s": n / t, "ms": t * 1e3})
         t = timeit(lambda: oracle.batch(alg, data, stride=length, length=length,
                                         n=n, nthreads=1))
-        res.append({"stage": f"CPU digest {name} (oracle, 1 core = test/sign.c shape)",
+        res.append({"key": f"cpu_digest_{name.lower()}_1core",
+                    "stage": f"CPU digest {name} (oracle, 1 core = test/sign.c shape)",
                     "payloads_per_s": n / t, "ms": t * 1e3})
     sigs = (Sig * n)()
     valid = (ctypes.c_int * n)()
@@ -96,12 +112,18 @@ def main():
         t_c = min(t_c, time.perf_counter() - t0)
     t_v = timeit(validate, reps=2)
     assert all(v == 1 for v in valid)
-    res.append({"stage": f"net2_signature_create_batch SHA512+ECDSA-P521, {threads} threads",
+    res.append({"key": "signature_create_batch",
+                "stage": f"net2_signature_create_batch SHA512+ECDSA-P521, {threads} threads",
                 "payloads_per_s": n / t_c, "ms": t_c * 1e3})
-    res.append({"stage": f"net2_signature_validate_batch SHA512+ECDSA-P521, {threads} threads",
+    res.append({"key": "signature_validate_batch",
+                "stage": f"net2_signature_validate_batch SHA512+ECDSA-P521, {threads} threads",
                 "payloads_per_s": n / t_v, "ms": t_v * 1e3})
     free_all()
-    for r in res:
+    return res
+
+
+def main():
+    for r in stages():
         r["config"] = "4096 x 1 KiB payloads (BASELINE configs[0] shape)"
         print(json.dumps(r), flush=True)
 

@@ -8,7 +8,7 @@ for lib in default tools/ab/*.so; do
   timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "fixed or var or config or hmac" > gpurun_out/pytest_pair.log 2>&1
   rc=$?; echo "parity $tag rc=$rc"; tail -1 gpurun_out/pytest_pair.log; [ $rc -ne 0 ] && exit $rc
   for c in ${PMC_CFGS:-c2 c3}; do
-    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/fpair_${tag}_$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --prewarm-ms 100 --no-cpu-baseline > gpurun_out/fpair_${tag}_$c.log 2>&1
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/fpair_${tag}_$c -o run -- python3 bench.py --config $c --steps 3 --warmup 1 --prewarm-ms 100 --no-cpu-baseline --no-extras > gpurun_out/fpair_${tag}_$c.log 2>&1
     rc=$?; echo "pmc $tag $c rc=$rc"; [ $rc -ne 0 ] && exit $rc
   done
 done
