@@ -79,6 +79,17 @@ SIGNATURES = {
     "net2_ph_to_iv_dev": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
         ctypes.c_void_p, ctypes.c_void_p]),
+    "net2_packet_burst_workspace": (ctypes.c_size_t, [ctypes.c_uint64]),
+    "net2_packet_decode_burst": (ctypes.c_int, [
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+        ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "net2_packet_encode_burst": (ctypes.c_int, [
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_size_t, ctypes.c_void_p]),
     # include/net2/sha2.h: the streaming interface of src/sha2.c
     "net2_sha2_ctx_init": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p]),
     "net2_sha2_ctx_update": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p,

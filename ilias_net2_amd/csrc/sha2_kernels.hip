@@ -1035,14 +1035,10 @@ __global__ __launch_bounds__(64) void job_kernel(const uint8_t *__restrict__ sta
  * packet.n2t:89-95).  The reference loops until the IV is long enough;
  * ivlen <= 64 covers two rounds, each a single block (8 + 32 bytes < 56).
  */
-__global__ __launch_bounds__(256) void ph_iv_kernel(const uint32_t *__restrict__ seq,
-    const uint32_t *__restrict__ flags, uint64_t n, uint32_t ivlen,
-    uint8_t *__restrict__ out)
+/* The IV of one header into out[0 .. ivlen) (ivlen <= 64). */
+__device__ __forceinline__ void ph_iv_one(uint32_t s, uint32_t f,
+    uint32_t ivlen, uint8_t *o)
 {
-	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	if (i >= n)
-		return;
-	const uint32_t s = seq[i], f = flags[i];
 	uint32_t d[16];
 	uint32_t st[8], w[16];
 #pragma unroll
@@ -1072,9 +1068,125 @@ __global__ __launch_bounds__(256) void ph_iv_kernel(const uint32_t *__restrict__
 		for (int j = 0; j < 8; j++)
 			d[8 * r + j] = st[j];
 	}
-	uint8_t *o = out + i * ivlen;
 	for (uint32_t b = 0; b < ivlen; b++)
 		o[b] = (uint8_t)(d[b >> 2] >> (24 - 8 * (b & 3)));
+}
+
+__global__ __launch_bounds__(256) void ph_iv_kernel(const uint32_t *__restrict__ seq,
+    const uint32_t *__restrict__ flags, uint64_t n, uint32_t ivlen,
+    uint8_t *__restrict__ out)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n)
+		return;
+	ph_iv_one(seq[i], flags[i], ivlen, out + i * ivlen);
+}
+
+/* ---- packet bursts: the hash steps of net2_packet_encode / decode ---------- */
+
+/*
+ * A datagram on the wire is the packet header (uint32 seq, uint32 flags,
+ * big-endian: cp_packet_header, types/packet.n2t:89-97), then -- when
+ * PH_SIGNED -- the HMAC of the rest (prepended last by net2_packet_encode,
+ * :417-426, removed first by net2_packet_decode, :233-243), then the
+ * payload (encrypted when PH_ENCRYPTED).  burst_prep_kernel does the
+ * per-datagram bookkeeping of those functions for a whole burst and points
+ * the HMAC kernel at each datagram's "hash field || payload" region;
+ * burst_final_kernel folds the HMAC verdicts in and derives the IVs.
+ *
+ * status byte: the NET2_P{EN,DE}CODE_* code, | BURST_VERIFY when the HMAC
+ * verdict of the region decides it.
+ */
+#define BURST_VERIFY 0x80u
+#define PKT_PH_ENCRYPTED 0x00000001u	/* types/packet.n2t:27 */
+#define PKT_PH_SIGNED 0x00000002u	/* types/packet.n2t:28 */
+#define PKT_OK 0
+#define PKT_RESOURCE 1
+#define PKT_BAD 2
+#define PKT_UNSAFE 3
+
+__device__ __forceinline__ uint32_t load_be32_bytes(const uint8_t *p)
+{
+	return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) |
+	    ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+
+__global__ __launch_bounds__(256) void burst_prep_kernel(uint8_t *__restrict__ base,
+    const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
+    uint64_t n, int encode, int hash_set, int enc_set, uint32_t hashlen,
+    const uint32_t *__restrict__ seq_in, const uint32_t *__restrict__ flags_in,
+    uint32_t *__restrict__ seq_out, uint32_t *__restrict__ flags_out,
+    uint64_t *__restrict__ sub_off, uint32_t *__restrict__ sub_len,
+    uint8_t *__restrict__ status)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n)
+		return;
+	const uint64_t off = offsets[i];
+	const uint32_t len = lens[i];
+	uint8_t *p = base + off;
+	uint32_t seq, fl, st = PKT_OK, sl = 0;
+	if (encode) {
+		seq = seq_in[i];
+		fl = flags_in[i];
+	} else if (len < 8) {		/* cp_packet_header decode fails, :196-198 */
+		seq = fl = 0;
+		st = PKT_BAD;
+	} else {
+		seq = load_be32_bytes(p);
+		fl = load_be32_bytes(p + 4);
+	}
+	const bool do_sign = (fl & PKT_PH_SIGNED) != 0;
+	const bool do_cryp = (fl & PKT_PH_ENCRYPTED) != 0;
+	if (st == PKT_OK) {
+		/* flags against the negotiated keys: decode :217-221, encode
+		 * :364-370 (which also refuses a flag without its key) */
+		if ((!do_sign && hash_set) || (!do_cryp && enc_set) ||
+		    (encode && ((do_sign && !hash_set) || (do_cryp && !enc_set))))
+			st = PKT_UNSAFE;
+	}
+	if (st == PKT_OK && encode) {
+		if (len < 8 + (do_sign ? hashlen : 0)) {
+			st = PKT_RESOURCE;	/* the slot has no room for them */
+		} else {
+			for (int b = 0; b < 4; b++) {
+				p[b] = (uint8_t)(seq >> (24 - 8 * b));
+				p[4 + b] = (uint8_t)(fl >> (24 - 8 * b));
+			}
+			if (do_sign)
+				sl = len - 8;	/* hash field || payload */
+		}
+	} else if (st == PKT_OK && do_sign && hash_set) {
+		sl = len - 8;		/* supplied hash || payload, :233-257 */
+		st |= BURST_VERIFY;
+	}
+	/* an empty region stays inside the datagram (a runt at the end of the
+	 * buffer has no bytes at off + 8) */
+	sub_off[i] = sl != 0 ? off + 8 : off;
+	sub_len[i] = sl;
+	status[i] = (uint8_t)st;
+	if (seq_out != nullptr) {
+		seq_out[i] = seq;
+		flags_out[i] = fl;
+	}
+}
+
+__global__ __launch_bounds__(256) void burst_final_kernel(uint64_t n,
+    const uint8_t *__restrict__ status, const uint8_t *__restrict__ verdict,
+    const uint32_t *__restrict__ seq, const uint32_t *__restrict__ flags,
+    uint32_t ivlen, uint8_t *__restrict__ iv, uint8_t *__restrict__ result)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n)
+		return;
+	uint32_t st = status[i];
+	if (st & BURST_VERIFY)		/* net2_buffer_cmp, :253-257 */
+		st = verdict[i] == 0 ? PKT_OK : PKT_BAD;
+	/* an encrypted datagram's IV from its header, :263-279 */
+	if (st == PKT_OK && iv != nullptr && ivlen > 0 &&
+	    (flags[i] & PKT_PH_ENCRYPTED))
+		ph_iv_one(seq[i], flags[i], ivlen, iv + i * ivlen);
+	result[i] = (uint8_t)st;
 }
 
 /* ---- length binning (counting sort by block count, longest first) ---- */
@@ -1540,6 +1652,29 @@ hipError_t net2_launch_jobs(const uint8_t *stage, const Net2Job *jobs,
 	if (n512 > 0)
 		job_kernel<Sha512><<<(n512 + 63) / 64, 64, 0, s>>>(stage,
 		    jobs + n256, n512, out + 64 * (size_t)n256, done);
+	return hipGetLastError();
+}
+
+hipError_t net2_launch_burst_prep(uint8_t *base, const uint64_t *offsets,
+    const uint32_t *lens, uint64_t n, int encode, int hash_set, int enc_set,
+    uint32_t hashlen, const uint32_t *seq_in, const uint32_t *flags_in,
+    uint32_t *seq_out, uint32_t *flags_out, uint64_t *sub_off,
+    uint32_t *sub_len, uint8_t *status, hipStream_t s)
+{
+	burst_prep_kernel<<<grid_for(n), 256, 0, s>>>(base, offsets, lens, n,
+	    encode, hash_set, enc_set, hashlen, seq_in, flags_in, seq_out,
+	    flags_out, sub_off, sub_len, status);
+	return hipGetLastError();
+}
+
+hipError_t net2_launch_burst_final(uint64_t n, const uint8_t *status,
+    const uint8_t *verdict, const uint32_t *seq, const uint32_t *flags,
+    uint32_t ivlen, uint8_t *iv, uint8_t *result, hipStream_t s)
+{
+	if (ivlen > 64)
+		return hipErrorInvalidValue;
+	burst_final_kernel<<<grid_for(n), 256, 0, s>>>(n, status, verdict, seq,
+	    flags, ivlen, iv, result);
 	return hipGetLastError();
 }
 

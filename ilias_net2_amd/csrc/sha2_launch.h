@@ -74,6 +74,20 @@ hipError_t net2_launch_jobs(const uint8_t *stage, const Net2Job *jobs,
     uint32_t n256, uint32_t n512, uint8_t *out, uint32_t *done,
     hipStream_t s);
 
+/*
+ * Packet bursts (net2_packet_{encode,decode}_burst): per-datagram header
+ * bookkeeping (prep) and the fold of HMAC verdicts + IV derivation (final);
+ * see sha2_kernels.hip.
+ */
+hipError_t net2_launch_burst_prep(uint8_t *base, const uint64_t *offsets,
+    const uint32_t *lens, uint64_t n, int encode, int hash_set, int enc_set,
+    uint32_t hashlen, const uint32_t *seq_in, const uint32_t *flags_in,
+    uint32_t *seq_out, uint32_t *flags_out, uint64_t *sub_off,
+    uint32_t *sub_len, uint8_t *status, hipStream_t s);
+hipError_t net2_launch_burst_final(uint64_t n, const uint8_t *status,
+    const uint8_t *verdict, const uint32_t *seq, const uint32_t *flags,
+    uint32_t ivlen, uint8_t *iv, uint8_t *result, hipStream_t s);
+
 /* Packet-header IVs (ivlen <= 64): out = n x ivlen bytes. */
 hipError_t net2_launch_ph_iv(const uint32_t *seq, const uint32_t *flags,
     uint64_t n, uint32_t ivlen, uint8_t *out, hipStream_t s);

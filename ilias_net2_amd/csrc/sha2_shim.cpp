@@ -949,3 +949,133 @@ NET2_EXPORT int net2_ph_to_iv_dev(const uint32_t *d_seq,
 	    (hipStream_t)stream));
 	return 0;
 }
+
+/* ---- packet bursts (include/net2/packet.h) --------------------------------- */
+
+namespace {
+
+/* Workspace of a burst, carved in this order, every piece 16-byte aligned:
+ * region offsets and lengths for the HMAC kernel, status and verdict bytes,
+ * decoded headers, the binning scratch. */
+struct BurstWs {
+	uint64_t *sub_off;
+	uint32_t *sub_len;
+	uint8_t *status, *verdict;
+	uint32_t *seq, *flags;
+	uint32_t *bin;
+};
+
+size_t a16(size_t x)
+{
+	return (x + 15) & ~(size_t)15;
+}
+
+size_t burst_layout(uint64_t n, uint8_t *base, BurstWs *w)
+{
+	size_t at = 0;
+	auto take = [&](size_t bytes) {
+		uint8_t *p = base ? base + at : nullptr;
+		at += a16(bytes);
+		return p;
+	};
+	uint64_t *so = (uint64_t *)take(8 * n);
+	uint32_t *sl = (uint32_t *)take(4 * n);
+	uint8_t *st = take(n);
+	uint8_t *vd = take(n);
+	uint32_t *sq = (uint32_t *)take(4 * n);
+	uint32_t *fl = (uint32_t *)take(4 * n);
+	uint32_t *bn = (uint32_t *)take((2 * (size_t)NET2_SHA2_NBINS + n) * 4);
+	if (w != nullptr)
+		*w = { so, sl, st, vd, sq, fl, bn };
+	return at;
+}
+
+/* hash_alg 0 (none) or an HMAC row with its key; ivlen <= 64 */
+int check_burst_args(int hash_alg, const void *key, size_t keylen,
+    uint32_t ivlen, const void *d_base, const uint64_t *d_offsets,
+    const uint32_t *d_lens, uint64_t n, const uint8_t *d_result,
+    const void *d_ws, size_t ws_bytes)
+{
+	if (hash_alg != NET2_HASH_NIL && (hash_alg < NET2_HASH_HMAC_SHA256 ||
+	    hash_alg > NET2_HASH_HMAC_SHA512))
+		return EINVAL;
+	if (hash_alg != NET2_HASH_NIL && ((size_t)kRows[hash_alg].keylen !=
+	    keylen || key == nullptr))
+		return EINVAL;
+	if (ivlen > 64)
+		return EINVAL;
+	if (n == 0)
+		return 0;
+	if (d_base == nullptr || d_offsets == nullptr || d_lens == nullptr ||
+	    d_result == nullptr || d_ws == nullptr || n > UINT32_MAX)
+		return EINVAL;
+	if (ws_bytes < burst_layout(n, nullptr, nullptr) ||
+	    ((uintptr_t)d_ws & 15) != 0)
+		return EINVAL;
+	return check_current_device();
+}
+
+}	/* namespace */
+
+NET2_EXPORT size_t net2_packet_burst_workspace(uint64_t n)
+{
+	return burst_layout(n, nullptr, nullptr);
+}
+
+NET2_EXPORT int net2_packet_decode_burst(int hash_alg, const void *hash_key,
+    size_t hash_keylen, int enc_alg, uint32_t ivlen, const void *d_base,
+    const uint64_t *d_offsets, const uint32_t *d_lens, uint64_t n,
+    uint8_t *d_result, void *d_iv, uint32_t *d_seq, uint32_t *d_flags,
+    void *d_ws, size_t ws_bytes, void *stream)
+{
+	int rc = check_burst_args(hash_alg, hash_key, hash_keylen, ivlen, d_base,
+	    d_offsets, d_lens, n, d_result, d_ws, ws_bytes);
+	if (rc != 0 || n == 0)
+		return rc;
+	if ((d_seq == nullptr) != (d_flags == nullptr))
+		return EINVAL;
+	BurstWs w;
+	burst_layout(n, (uint8_t *)d_ws, &w);
+	uint32_t *seq = d_seq ? d_seq : w.seq, *flags = d_flags ? d_flags : w.flags;
+	hipStream_t s = (hipStream_t)stream;
+	const int hash_set = hash_alg != NET2_HASH_NIL;
+	HIP_TRY(net2_launch_burst_prep((uint8_t *)d_base, d_offsets, d_lens, n,
+	    0, hash_set, enc_alg != 0, hash_set ? kRows[hash_alg].hashlen : 0,
+	    nullptr, nullptr, seq, flags, w.sub_off, w.sub_len, w.status, s));
+	if (hash_set)
+		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)hash_key,
+		    hash_keylen, (const uint8_t *)d_base, w.sub_off, w.sub_len, 0,
+		    0, n, w.verdict, w.bin, s, NET2_HMAC_MODE_VERIFY));
+	HIP_TRY(net2_launch_burst_final(n, w.status, w.verdict, seq, flags,
+	    enc_alg != 0 ? ivlen : 0, (uint8_t *)d_iv, d_result, s));
+	return 0;
+}
+
+NET2_EXPORT int net2_packet_encode_burst(int hash_alg, const void *hash_key,
+    size_t hash_keylen, int enc_alg, const uint32_t *d_seq,
+    const uint32_t *d_flags, void *d_base, const uint64_t *d_offsets,
+    const uint32_t *d_lens, uint64_t n, uint8_t *d_result, void *d_ws,
+    size_t ws_bytes, void *stream)
+{
+	int rc = check_burst_args(hash_alg, hash_key, hash_keylen, 0, d_base,
+	    d_offsets, d_lens, n, d_result, d_ws, ws_bytes);
+	if (rc != 0 || n == 0)
+		return rc;
+	if (d_seq == nullptr || d_flags == nullptr)
+		return EINVAL;
+	BurstWs w;
+	burst_layout(n, (uint8_t *)d_ws, &w);
+	hipStream_t s = (hipStream_t)stream;
+	const int hash_set = hash_alg != NET2_HASH_NIL;
+	HIP_TRY(net2_launch_burst_prep((uint8_t *)d_base, d_offsets, d_lens, n,
+	    1, hash_set, enc_alg != 0, hash_set ? kRows[hash_alg].hashlen : 0,
+	    d_seq, d_flags, nullptr, nullptr, w.sub_off, w.sub_len, w.status, s));
+	if (hash_set)
+		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)hash_key,
+		    hash_keylen, (const uint8_t *)d_base, w.sub_off, w.sub_len, 0,
+		    0, n, (uint8_t *)d_base, w.bin, s, NET2_HMAC_MODE_SIGN));
+	HIP_TRY(net2_launch_burst_final(n, w.status, nullptr, d_seq, d_flags, 0,
+	    nullptr, d_result, s));
+	return 0;
+}
+

@@ -1,9 +1,9 @@
 /*
  * net2/packet.h -- the SHA-2 uses of the packet codec (types/packet.n2t)
  * on the MI355X path: IV derivation from a packet header
- * (net2_ph_to_iv, packet.n2t:100-158).  The per-datagram keyed hash of
- * net2_packet_encode/decode (packet.n2t:226-257, 410-427) is net2_hmac_dev
- * in net2/hash.h.
+ * (net2_ph_to_iv, packet.n2t:100-158), and the hash steps of
+ * net2_packet_encode / net2_packet_decode (packet.n2t:341-463 / :170-336)
+ * for whole bursts of datagrams under one connection's keys.
  */
 #ifndef NET2_PACKET_H
 #define NET2_PACKET_H
@@ -39,6 +39,67 @@ int net2_ph_to_iv(const struct net2_packet_header *ph, size_t ivlen,
  */
 int net2_ph_to_iv_dev(const uint32_t *d_seq, const uint32_t *d_flags,
     uint64_t n, uint32_t ivlen, void *d_iv, void *stream);
+
+/* Packet header flags used here (types/packet.n2t:27-28) and the result
+ * codes of net2_packet_decode / _encode (:44-47, :53-56). */
+#define NET2_PH_ENCRYPTED	0x00000001
+#define NET2_PH_SIGNED		0x00000002
+#define NET2_PDECODE_OK		0
+#define NET2_PDECODE_RESOURCE	1
+#define NET2_PDECODE_BAD	2
+#define NET2_PDECODE_UNSAFE	3
+#define NET2_PENCODE_OK		0
+#define NET2_PENCODE_RESOURCE	1
+#define NET2_PENCODE_BAD	2
+#define NET2_PENCODE_UNSAFE	3
+
+/* Device scratch (bytes, 16-byte aligned) of a burst of n datagrams. */
+size_t net2_packet_burst_workspace(uint64_t n);
+
+/*
+ * RX: the hash steps of net2_packet_decode for a burst of n received
+ * datagrams under one connection's rx keys, device-resident and
+ * asynchronous on `stream` (one stream, no host synchronisation).
+ * Datagram i = d_base[d_offsets[i] .. + d_lens[i]) as it came off the wire:
+ * 8-byte header (seq, flags big-endian), then the HMAC field when
+ * PH_SIGNED, then the payload.  hash_alg is the negotiated keyed hash
+ * (HMAC row 4..6, key of its registry length) or 0 for none; enc_alg != 0
+ * when an encryption key is negotiated, ivlen its IV length (<= 64;
+ * AES-256-CBC: 16, src/enc.c:72-73).  Per datagram, as packet.n2t does:
+ *   - shorter than the header: NET2_PDECODE_BAD (:196-198);
+ *   - PH_SIGNED / PH_ENCRYPTED missing while the key is set:
+ *     NET2_PDECODE_UNSAFE (:215-221);
+ *   - PH_SIGNED: the hash field is compared with HMAC(key, rest); too
+ *     short or unequal: NET2_PDECODE_BAD (:226-258);
+ *   - PH_ENCRYPTED and OK: the IV for the decryption step,
+ *     net2_ph_to_iv (:263-279), to d_iv + i * ivlen (d_iv may be NULL).
+ * d_result[i] receives the code; d_seq / d_flags (both or neither) the
+ * decoded header.  The window check, the decryption itself and the key
+ * commit (:200-206, :283-313) stay with the caller.
+ */
+int net2_packet_decode_burst(int hash_alg, const void *hash_key,
+    size_t hash_keylen, int enc_alg, uint32_t ivlen, const void *d_base,
+    const uint64_t *d_offsets, const uint32_t *d_lens, uint64_t n,
+    uint8_t *d_result, void *d_iv, uint32_t *d_seq, uint32_t *d_flags,
+    void *d_ws, size_t ws_bytes, void *stream);
+
+/*
+ * TX: the hash steps of net2_packet_encode for a burst.  Datagram slot i =
+ * d_base[d_offsets[i] .. + d_lens[i]) holds, on entry, 8 bytes for the
+ * header, then hashlen reserved bytes when d_flags[i] has PH_SIGNED (as
+ * connection.c:336-339 reserves them), then the payload -- already
+ * encrypted when PH_ENCRYPTED (its IV comes from net2_ph_to_iv_dev first).
+ * The flags are checked against the keys both ways (NET2_PENCODE_UNSAFE,
+ * :364-370); then the header (d_seq[i], d_flags[i]) is written big-endian
+ * and, when PH_SIGNED, the HMAC of the payload into the reserved field
+ * (:410-443).  A slot too short for header and field gets
+ * NET2_PENCODE_RESOURCE and is left untouched.  Codes to d_result.
+ */
+int net2_packet_encode_burst(int hash_alg, const void *hash_key,
+    size_t hash_keylen, int enc_alg, const uint32_t *d_seq,
+    const uint32_t *d_flags, void *d_base, const uint64_t *d_offsets,
+    const uint32_t *d_lens, uint64_t n, uint8_t *d_result, void *d_ws,
+    size_t ws_bytes, void *stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,193 @@
+"""Bursts of datagrams through the hash steps of net2_packet_encode / decode
+(types/packet.n2t:341-463 / :170-336): net2_packet_encode_burst and
+net2_packet_decode_burst against a line-by-line Python restatement of those
+functions over the oracle's HMAC and net2_ph_to_iv (oracle/sha2_oracle.c).
+
+Every burst mixes PH_SIGNED / PH_ENCRYPTED / other flag bits, runts shorter
+than the header, signed datagrams too short for their hash field, tampered
+payloads and hash fields, and flag / key mismatches (UNSAFE), under each
+key set-up the negotiation can produce (keyed hash and cipher, either one,
+neither).
+"""
+import struct
+
+import numpy as np
+import pytest
+
+import synth
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+PH_ENCRYPTED, PH_SIGNED, PH_ALTKEY = 0x1, 0x2, 0x80000000
+OK, RESOURCE, BAD, UNSAFE = 0, 1, 2, 3
+HL = {0: 0, 4: 32, 5: 48, 6: 64}
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a GPU (HIP device not visible)")
+    from ilias_net2_amd import _lib
+    assert _lib.device_count() >= 1
+    return torch.device("cuda:0")
+
+
+def ref_decode(dg, hash_alg, key, enc_set, ivlen, oracle_mod):
+    """net2_packet_decode (packet.n2t:170-336), hash steps only."""
+    if len(dg) < 8:                                   # :196-198
+        return BAD, None, None
+    seq, fl = struct.unpack(">II", dg[:8])
+    do_sign, do_cryp = fl & PH_SIGNED, fl & PH_ENCRYPTED
+    if (not do_sign and hash_alg) or (not do_cryp and enc_set):   # :217-221
+        return UNSAFE, (seq, fl), None
+    rest = dg[8:]
+    if do_sign:                                       # :226-258
+        hl = HL[hash_alg]
+        if len(rest) < hl:
+            return BAD, (seq, fl), None
+        supplied, msg = rest[:hl], rest[hl:]
+        calc = oracle_mod.hmac(hash_alg, key, msg) if hash_alg else b""
+        if supplied != calc:
+            return BAD, (seq, fl), None
+    iv = None
+    if do_cryp and enc_set and ivlen:                 # :263-279
+        iv = oracle_mod.ph_to_iv(seq, fl, ivlen)
+    return OK, (seq, fl), iv
+
+
+def ref_encode(slot, seq, fl, hash_alg, key, enc_set, oracle_mod):
+    """net2_packet_encode (packet.n2t:341-463) on a slot laid out as header
+    || reserved hash field (PH_SIGNED) || payload; returns (code, bytes)."""
+    do_sign, do_cryp = fl & PH_SIGNED, fl & PH_ENCRYPTED
+    if ((not do_sign and hash_alg) or (not do_cryp and enc_set) or
+            (do_sign and not hash_alg) or (do_cryp and not enc_set)):  # :364-370
+        return UNSAFE, slot
+    hl = HL[hash_alg] if do_sign else 0
+    if len(slot) < 8 + hl:
+        return RESOURCE, slot
+    payload = slot[8 + hl:]
+    field = oracle_mod.hmac(hash_alg, key, payload) if do_sign else b""
+    return OK, struct.pack(">II", seq, fl) + field + payload
+
+
+def _dev(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+SETUPS = [(6, True, 16), (4, True, 16), (5, False, 0), (0, True, 32),
+          (0, False, 0), (6, True, 64)]
+
+
+@pytest.mark.parametrize("hash_alg,enc_set,ivlen", SETUPS)
+def test_encode_then_decode_burst(dev, oracle_mod, hash_alg, enc_set, ivlen):
+    from ilias_net2_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(1000 + 10 * hash_alg + ivlen + enc_set)
+    n = 3001
+    key = rng.integers(0, 256, HL[hash_alg], dtype=np.uint8).tobytes()
+    want_flags = (PH_SIGNED if hash_alg else 0) | (PH_ENCRYPTED if enc_set else 0)
+    # mostly the flags the keys call for; some wrong ones, some extra bits
+    flags = np.full(n, want_flags, dtype=np.uint32)
+    pick = rng.random(n)
+    flags[pick < 0.1] ^= PH_SIGNED
+    flags[(pick >= 0.1) & (pick < 0.2)] ^= PH_ENCRYPTED
+    flags[(pick >= 0.2) & (pick < 0.3)] |= PH_ALTKEY | 0x10
+    seq = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    plen = rng.choice([0, 1, 17, 64, 500, 1472], n)
+    hl = np.where(flags & PH_SIGNED, HL[hash_alg], 0)
+    slot = (8 + hl + plen).astype(np.uint32)
+    short = rng.random(n) < 0.03              # slots with no room
+    slot[short] = rng.integers(0, 8 + HL[hash_alg] + 1, short.sum())
+    data, offs = synth.packed(1100 + hash_alg, slot, align=1, gap=3)
+    kb = (key or b"\0")
+
+    # ---- TX -------------------------------------------------------------
+    d = _dev(data, dev)
+    o, ln = _dev(offs.astype(np.int64), dev), _dev(slot.astype(np.int32), dev)
+    ds, df = _dev(seq.view(np.int32), dev), _dev(flags.view(np.int32), dev)
+    res = torch.full((n,), 9, dtype=torch.uint8, device=dev)
+    ws = torch.empty(L.net2_packet_burst_workspace(n), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    rc = L.net2_packet_encode_burst(hash_alg, kb, len(key), int(enc_set), ds.data_ptr(),
+                                    df.data_ptr(), d.data_ptr(), o.data_ptr(),
+                                    ln.data_ptr(), n, res.data_ptr(), ws.data_ptr(),
+                                    ws.numel(), st)
+    assert rc == 0
+    tx = d.cpu().numpy()
+    got = res.cpu().numpy()
+    for i in range(n):
+        a, b = int(offs[i]), int(offs[i]) + int(slot[i])
+        code, want = ref_encode(data[a:b].tobytes(), int(seq[i]), int(flags[i]),
+                                hash_alg, key, enc_set, oracle_mod)
+        assert got[i] == code, (i, got[i], code)
+        assert tx[a:b].tobytes() == want, i
+
+    # ---- RX: what TX produced, plus runts and tampered datagrams ---------
+    rx = tx.copy()
+    lens = slot.copy()
+    tamper = rng.random(n)
+    for i in range(n):
+        a = int(offs[i])
+        if tamper[i] < 0.05 and lens[i] > 8:       # flip a byte past the header
+            j = a + 8 + int(rng.integers(0, lens[i] - 8))
+            rx[j] ^= 0x40
+        elif tamper[i] < 0.08:                     # runt
+            lens[i] = int(rng.integers(0, 8))
+    d2 = _dev(rx, dev)
+    ln2 = _dev(lens.astype(np.int32), dev)
+    res.fill_(9)
+    iv = torch.zeros((n, max(ivlen, 1)), dtype=torch.uint8, device=dev)
+    oseq = torch.zeros(n, dtype=torch.int32, device=dev)
+    ofl = torch.zeros(n, dtype=torch.int32, device=dev)
+    rc = L.net2_packet_decode_burst(hash_alg, kb, len(key), int(enc_set), ivlen,
+                                    d2.data_ptr(), o.data_ptr(), ln2.data_ptr(), n,
+                                    res.data_ptr(), iv.data_ptr() if ivlen else None,
+                                    oseq.data_ptr(), ofl.data_ptr(), ws.data_ptr(),
+                                    ws.numel(), st)
+    assert rc == 0
+    got = res.cpu().numpy()
+    giv = iv.cpu().numpy()
+    gseq = oseq.cpu().numpy().view(np.uint32)
+    gfl = ofl.cpu().numpy().view(np.uint32)
+    counts = {}
+    for i in range(n):
+        a = int(offs[i])
+        dg = rx[a:a + int(lens[i])].tobytes()
+        code, hdr, want_iv = ref_decode(dg, hash_alg, key, enc_set, ivlen, oracle_mod)
+        counts[code] = counts.get(code, 0) + 1
+        assert got[i] == code, (i, got[i], code)
+        if hdr is not None:
+            assert (gseq[i], gfl[i]) == hdr, i
+        if want_iv is not None:
+            assert giv[i, :ivlen].tobytes() == want_iv, i
+    # every outcome the set-up allows actually occurred
+    assert counts.get(OK, 0) > n // 2 and counts.get(BAD, 0) > 0
+    if hash_alg or enc_set:
+        assert counts.get(UNSAFE, 0) > 0
+
+
+def test_burst_argument_errors(dev):
+    from ilias_net2_amd import _lib
+    import errno
+    L = _lib.lib()
+    t = torch.zeros(256, dtype=torch.uint8, device=dev)
+    p = t.data_ptr()
+    ws = L.net2_packet_burst_workspace(4)
+    w = torch.zeros(ws, dtype=torch.uint8, device=dev)
+    key = b"k" * 64
+    # unkeyed row, wrong key length, ivlen > 64, workspace too small
+    assert L.net2_packet_decode_burst(1, key, 0, 0, 0, p, p, p, 4, p, None, None,
+                                      None, w.data_ptr(), ws, None) == errno.EINVAL
+    assert L.net2_packet_decode_burst(4, key, 31, 0, 0, p, p, p, 4, p, None, None,
+                                      None, w.data_ptr(), ws, None) == errno.EINVAL
+    assert L.net2_packet_decode_burst(0, None, 0, 1, 65, p, p, p, 4, p, p, None,
+                                      None, w.data_ptr(), ws, None) == errno.EINVAL
+    assert L.net2_packet_decode_burst(0, None, 0, 0, 0, p, p, p, 4, p, None, None,
+                                      None, w.data_ptr(), ws - 1, None) == errno.EINVAL
+    assert L.net2_packet_encode_burst(4, key, 32, 0, None, None, p, p, p, 4, p,
+                                      w.data_ptr(), ws, None) == errno.EINVAL
+    # an empty burst is a no-op
+    assert L.net2_packet_decode_burst(0, None, 0, 0, 0, None, None, None, 0, None,
+                                      None, None, None, None, 0, None) == 0
