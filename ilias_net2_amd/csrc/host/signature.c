@@ -11,6 +11,7 @@
  */
 #include "../../../include/net2/signature.h"
 #include "../../../include/net2/hash.h"
+#include "signature_int.h"
 
 #include <errno.h>
 #include <pthread.h>
@@ -44,8 +45,9 @@ net2_signature_deinit(struct net2_signature *s)
 	s->datalen = 0;
 }
 
-/* Fill s from an already computed digest (signature.n2t:74-100). */
-static int
+/* Fill s from an already computed digest (signature.n2t:74-100); shared
+ * with the tick-batched carver step (signed_carver.c), hidden. */
+int
 sign_digest(struct net2_signature *s, const uint8_t *digest, size_t dlen,
     const char *hash_name, struct net2_sign_ctx *sign)
 {

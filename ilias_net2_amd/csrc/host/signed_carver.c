@@ -1,0 +1,495 @@
+/*
+ * signed_carver.c -- the hashing and signing steps of src/signed_carver.c,
+ * batched per workq tick (include/net2/signed_carver.h).
+ *
+ * One tick: (1) every payload of the tick, from new carvers and from
+ * combiner checks alike, is hashed once -- all payloads of one hash
+ * algorithm in one net2_sha2_batch call (the reference hashes each payload
+ * once per sign context, src/signed_carver.c:407-411 -> signature.n2t:92);
+ * (2) the ECDSA work -- num_signatures signatures per carver (:407-432),
+ * one verification per check (:305-319) -- is spread over host threads.
+ */
+#include "../../../include/net2/signed_carver.h"
+#include "../../../include/net2/hash.h"
+#include "signature_int.h"
+
+#include <errno.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#define NET2_EXPORT __attribute__((visibility("default")))
+
+/* ---- one tick -------------------------------------------------------- */
+
+/* One payload to hash: where its digest goes. */
+struct payload_ref {
+	const struct iovec	*iov;
+	size_t			 iovcnt;
+	int			 alg;		/* 1..3, or < 0: not hashed */
+	uint8_t			*digest;	/* 64 bytes */
+	int			*rc;		/* set on a hash failure */
+};
+
+static size_t
+iov_len(const struct iovec *iov, size_t n)
+{
+	size_t t = 0;
+
+	for (size_t i = 0; i < n; i++)
+		t += iov[i].iov_len;
+	return t;
+}
+
+/*
+ * Hash every payload of algorithm alg in one net2_sha2_batch call.
+ * Single-segment payloads are passed in place, as offsets from the lowest
+ * payload address; multi-segment ones are gathered first.
+ */
+static int
+hash_group(struct payload_ref *p, size_t np, int alg)
+{
+	size_t m = 0, gathered = 0;
+	uintptr_t lo = UINTPTR_MAX;
+	uint64_t *offs = NULL;
+	uint32_t *lens = NULL;
+	uint8_t *dig = NULL, *gbuf = NULL, *at;
+	const int hl = net2_hash_gethashlen(alg);
+	int rc = 0;
+
+	for (size_t i = 0; i < np; i++) {
+		if (p[i].alg != alg)
+			continue;
+		m++;
+		if (p[i].iovcnt > 1)
+			gathered += iov_len(p[i].iov, p[i].iovcnt);
+	}
+	if (m == 0)
+		return 0;
+	offs = malloc(m * sizeof(*offs));
+	lens = malloc(m * sizeof(*lens));
+	dig = malloc(m * (size_t)hl);
+	gbuf = malloc(gathered ? gathered : 1);
+	if (offs == NULL || lens == NULL || dig == NULL || gbuf == NULL) {
+		rc = ENOMEM;
+		goto out;
+	}
+	/* the address of every payload's bytes, then offsets from the lowest */
+	at = gbuf;
+	m = 0;
+	for (size_t i = 0; i < np; i++) {
+		if (p[i].alg != alg)
+			continue;
+		const size_t len = iov_len(p[i].iov, p[i].iovcnt);
+		uintptr_t a;
+		if (len > UINT32_MAX) {
+			rc = EINVAL;
+			goto out;
+		}
+		if (p[i].iovcnt > 1) {
+			a = (uintptr_t)at;
+			for (size_t k = 0; k < p[i].iovcnt; k++) {
+				if (p[i].iov[k].iov_len)
+					memcpy(at, p[i].iov[k].iov_base,
+					    p[i].iov[k].iov_len);
+				at += p[i].iov[k].iov_len;
+			}
+		} else {
+			a = p[i].iovcnt == 1 ? (uintptr_t)p[i].iov[0].iov_base :
+			    (uintptr_t)gbuf;
+		}
+		offs[m] = a;
+		lens[m] = (uint32_t)len;
+		if (a < lo)
+			lo = a;
+		m++;
+	}
+	for (size_t k = 0; k < m; k++)
+		offs[k] -= lo;
+	rc = net2_sha2_batch(alg, (const void *)lo, offs, lens, 0, 0, m, dig,
+	    0);
+	if (rc == 0) {
+		m = 0;
+		for (size_t i = 0; i < np; i++)
+			if (p[i].alg == alg)
+				memcpy(p[i].digest, dig + (m++) * (size_t)hl,
+				    (size_t)hl);
+	}
+out:
+	if (rc != 0)
+		for (size_t i = 0; i < np; i++)
+			if (p[i].alg == alg && *p[i].rc == 0)
+				*p[i].rc = rc;
+	free(offs);
+	free(lens);
+	free(dig);
+	free(gbuf);
+	return rc;
+}
+
+/* ECDSA jobs: job j < nsig_jobs signs, the rest validate. */
+struct ecdsa_plan {
+	struct net2_sc_sign_req		*sreq;
+	size_t				 ns;
+	struct net2_sc_validate_req	*vreq;
+	size_t				 nv;
+	const uint8_t			*sdig;	/* ns x 64 */
+	const uint8_t			*vdig;	/* nv x 64 */
+	const int			*valg;	/* hash row per check, < 0 bad */
+	const size_t			*sjob;	/* prefix sums of num_signatures */
+	size_t				 nsig_jobs, njobs;
+};
+
+struct ecdsa_slice {
+	const struct ecdsa_plan	*pl;
+	size_t			 lo, hi;
+};
+
+/* request index of signature job j (binary search over the prefix sums) */
+static size_t
+sign_req_of(const struct ecdsa_plan *pl, size_t j)
+{
+	size_t a = 0, b = pl->ns;
+
+	while (b - a > 1) {
+		size_t c = (a + b) / 2;
+		if (pl->sjob[c] <= j)
+			a = c;
+		else
+			b = c;
+	}
+	return a;
+}
+
+static void *
+ecdsa_run(void *arg)
+{
+	const struct ecdsa_slice *sl = arg;
+	const struct ecdsa_plan *pl = sl->pl;
+
+	for (size_t j = sl->lo; j < sl->hi; j++) {
+		if (j < pl->nsig_jobs) {
+			const size_t r = sign_req_of(pl, j);
+			struct net2_sc_sign_req *q = &pl->sreq[r];
+			const size_t k = j - pl->sjob[r];
+			if (q->rc != 0)
+				continue;
+			int rc = sign_digest(&q->out[k], pl->sdig + 64 * r,
+			    (size_t)net2_hash_gethashlen(q->hash_alg),
+			    net2_hash_getname(q->hash_alg), q->signatures[k]);
+			if (rc != 0)
+				__atomic_store_n(&q->rc, rc, __ATOMIC_RELAXED);
+			continue;
+		}
+		const size_t v = j - pl->nsig_jobs;
+		struct net2_sc_validate_req *q = &pl->vreq[v];
+		if (pl->valg[v] < 0 || q->result != 0)
+			continue;
+		if (strcmp(net2_signctx_name(q->sctx), q->sig->sign_alg) != 0) {
+			q->result = EIO;	/* signature.n2t:155-158 -> :333-336 */
+			continue;
+		}
+		q->result = net2_signctx_validate(q->sctx, q->sig->data,
+		    q->sig->datalen, pl->vdig + 64 * v,
+		    (size_t)net2_hash_gethashlen(pl->valg[v])) == 1 ? 0 : EINVAL;
+	}
+	return NULL;
+}
+
+static void
+run_jobs(const struct ecdsa_plan *pl, int nthreads)
+{
+	struct ecdsa_slice sl[64];
+	pthread_t tid[64];
+	int t, started;
+
+	if (nthreads <= 0) {
+		long c = sysconf(_SC_NPROCESSORS_ONLN);
+		nthreads = c > 0 ? (int)c : 1;
+	}
+	if (nthreads > 64)
+		nthreads = 64;
+	if ((size_t)nthreads > pl->njobs)
+		nthreads = pl->njobs ? (int)pl->njobs : 1;
+	for (t = 0; t < nthreads; t++) {
+		sl[t].pl = pl;
+		sl[t].lo = pl->njobs * t / nthreads;
+		sl[t].hi = pl->njobs * (t + 1) / nthreads;
+	}
+	for (started = 1; started < nthreads; started++)
+		if (pthread_create(&tid[started], NULL, ecdsa_run,
+		    &sl[started]) != 0)
+			break;
+	ecdsa_run(&sl[0]);
+	for (t = started; t < nthreads; t++)	/* threads we could not start */
+		ecdsa_run(&sl[t]);
+	for (t = 1; t < started; t++)
+		pthread_join(tid[t], NULL);
+}
+
+/* validate_prologue of signature.c (signature.n2t:133-145): hash row of a
+ * decoded signature, or -1 when it cannot be validated */
+static int
+check_alg(const struct net2_sc_validate_req *q)
+{
+	int alg;
+
+	if (q->sig == NULL || q->sctx == NULL || q->sig->data == NULL ||
+	    q->sig->hash_alg == NULL || q->sig->sign_alg == NULL ||
+	    (q->payload == NULL && q->iovcnt > 0))
+		return -1;
+	if ((alg = net2_hash_findname(q->sig->hash_alg)) < 0 ||
+	    net2_hash_getkeylen(alg) != 0 || net2_hash_gethashlen(alg) <= 0)
+		return -1;
+	return alg;
+}
+
+static int
+tick(struct net2_sc_sign_req *sreq, size_t ns,
+    struct net2_sc_validate_req *vreq, size_t nv, int nthreads)
+{
+	struct payload_ref *p = NULL;
+	uint8_t *sdig = NULL, *vdig = NULL;
+	int *valg = NULL, rc = 0;
+	size_t *sjob = NULL, np = 0;
+	struct ecdsa_plan pl;
+
+	if (ns + nv == 0)
+		return 0;
+	p = calloc(ns + nv, sizeof(*p));
+	sdig = malloc(ns * 64 + 1);
+	vdig = malloc(nv * 64 + 1);
+	valg = malloc((nv + 1) * sizeof(*valg));
+	sjob = malloc((ns + 1) * sizeof(*sjob));
+	if (p == NULL || sdig == NULL || vdig == NULL || valg == NULL ||
+	    sjob == NULL) {
+		rc = ENOMEM;
+		for (size_t i = 0; i < ns; i++)
+			sreq[i].rc = ENOMEM;
+		for (size_t i = 0; i < nv; i++)
+			vreq[i].result = EIO;
+		goto out;
+	}
+	/* requests -> payloads to hash */
+	sjob[0] = 0;
+	for (size_t i = 0; i < ns; i++) {
+		struct net2_sc_sign_req *q = &sreq[i];
+		q->rc = 0;
+		if (q->out == NULL || (q->num_signatures > 0 &&
+		    q->signatures == NULL) || (q->payload == NULL &&
+		    q->iovcnt > 0) || net2_hash_getname(q->hash_alg) == NULL ||
+		    net2_hash_gethashlen(q->hash_alg) <= 0 ||
+		    net2_hash_getkeylen(q->hash_alg) != 0)
+			q->rc = EINVAL;		/* signature.n2t:69-72 */
+		else
+			memset(q->out, 0, q->num_signatures * sizeof(*q->out));
+		sjob[i + 1] = sjob[i] + (q->rc == 0 ? q->num_signatures : 0);
+		p[np++] = (struct payload_ref){ q->payload, q->iovcnt,
+		    q->rc == 0 ? q->hash_alg : -1, sdig + 64 * i, &q->rc };
+	}
+	for (size_t i = 0; i < nv; i++) {
+		struct net2_sc_validate_req *q = &vreq[i];
+		valg[i] = check_alg(q);
+		q->result = valg[i] < 0 ? EIO : 0;
+		p[np++] = (struct payload_ref){ q->payload, q->iovcnt, valg[i],
+		    vdig + 64 * i, &q->result };
+	}
+	/* one GPU batch per hash algorithm */
+	for (int alg = NET2_HASH_SHA256; alg <= NET2_HASH_SHA512; alg++) {
+		int r = hash_group(p, np, alg);
+		if (r != 0 && rc == 0)
+			rc = r;
+	}
+	for (size_t i = 0; i < nv; i++)
+		if (vreq[i].result != 0) {
+			vreq[i].result = EIO;	/* hash failure: :333-336 */
+			valg[i] = -1;
+		}
+	/* the ECDSA work on host threads */
+	pl.sreq = sreq;
+	pl.ns = ns;
+	pl.vreq = vreq;
+	pl.nv = nv;
+	pl.sdig = sdig;
+	pl.vdig = vdig;
+	pl.valg = valg;
+	pl.sjob = sjob;
+	pl.nsig_jobs = sjob[ns];
+	pl.njobs = sjob[ns] + nv;
+	if (pl.njobs > 0)
+		run_jobs(&pl, nthreads);
+	/* a carver whose signing failed keeps none of its signatures */
+	for (size_t i = 0; i < ns; i++)
+		if (sreq[i].rc != 0 && sreq[i].out != NULL &&
+		    sreq[i].rc != EINVAL)
+			for (uint32_t k = 0; k < sreq[i].num_signatures; k++)
+				net2_signature_deinit(&sreq[i].out[k]);
+	if (rc == 0 && ns > 0) {
+		/* the batch failed as a whole only if every carver failed */
+		int all = 1;
+		for (size_t i = 0; i < ns && all; i++)
+			all = sreq[i].rc != 0;
+		if (all && nv == 0)
+			rc = sreq[0].rc;
+	}
+out:
+	free(p);
+	free(sdig);
+	free(vdig);
+	free(valg);
+	free(sjob);
+	return rc;
+}
+
+NET2_EXPORT int
+net2_signed_carver_sign_tick(struct net2_sc_sign_req *reqs, size_t n,
+    int nthreads)
+{
+	if (n > 0 && reqs == NULL)
+		return EINVAL;
+	return tick(reqs, n, NULL, 0, nthreads);
+}
+
+NET2_EXPORT int
+net2_signed_combiner_validate_tick(struct net2_sc_validate_req *reqs,
+    size_t n, int nthreads)
+{
+	if (n > 0 && reqs == NULL)
+		return EINVAL;
+	return tick(NULL, 0, reqs, n, nthreads);
+}
+
+/* ---- the collector ---------------------------------------------------- */
+
+struct net2_sc_collector {
+	pthread_mutex_t			 mu;
+	int				 nthreads;
+	struct net2_sc_sign_req		**sign;
+	size_t				 nsign, capsign;
+	struct net2_sc_validate_req	**val;
+	size_t				 nval, capval;
+};
+
+NET2_EXPORT struct net2_sc_collector *
+net2_sc_collector_new(int nthreads)
+{
+	struct net2_sc_collector *c = calloc(1, sizeof(*c));
+
+	if (c == NULL)
+		return NULL;
+	if (pthread_mutex_init(&c->mu, NULL) != 0) {
+		free(c);
+		return NULL;
+	}
+	c->nthreads = nthreads;
+	return c;
+}
+
+NET2_EXPORT void
+net2_sc_collector_free(struct net2_sc_collector *c)
+{
+	if (c == NULL)
+		return;
+	pthread_mutex_destroy(&c->mu);
+	free(c->sign);
+	free(c->val);
+	free(c);
+}
+
+static int
+push(void ***arr, size_t *n, size_t *cap, void *item)
+{
+	if (*n == *cap) {
+		size_t nc = *cap ? 2 * *cap : 64;
+		void **na = realloc(*arr, nc * sizeof(*na));
+		if (na == NULL)
+			return ENOMEM;
+		*arr = na;
+		*cap = nc;
+	}
+	(*arr)[(*n)++] = item;
+	return 0;
+}
+
+NET2_EXPORT int
+net2_sc_collector_add_sign(struct net2_sc_collector *c,
+    struct net2_sc_sign_req *r)
+{
+	int rc;
+
+	if (c == NULL || r == NULL)
+		return EINVAL;
+	pthread_mutex_lock(&c->mu);
+	rc = push((void ***)&c->sign, &c->nsign, &c->capsign, r);
+	pthread_mutex_unlock(&c->mu);
+	return rc;
+}
+
+NET2_EXPORT int
+net2_sc_collector_add_validate(struct net2_sc_collector *c,
+    struct net2_sc_validate_req *r)
+{
+	int rc;
+
+	if (c == NULL || r == NULL)
+		return EINVAL;
+	pthread_mutex_lock(&c->mu);
+	rc = push((void ***)&c->val, &c->nval, &c->capval, r);
+	pthread_mutex_unlock(&c->mu);
+	return rc;
+}
+
+NET2_EXPORT int
+net2_sc_collector_tick(struct net2_sc_collector *c, size_t *nsign,
+    size_t *nvalidate)
+{
+	struct net2_sc_sign_req **sp, *sreq = NULL;
+	struct net2_sc_validate_req **vp, *vreq = NULL;
+	size_t ns, nv;
+	int rc;
+
+	if (c == NULL)
+		return EINVAL;
+	/* take the tick's requests; later adds go to the next tick */
+	pthread_mutex_lock(&c->mu);
+	sp = c->sign;
+	ns = c->nsign;
+	vp = c->val;
+	nv = c->nval;
+	c->sign = NULL;
+	c->nsign = c->capsign = 0;
+	c->val = NULL;
+	c->nval = c->capval = 0;
+	pthread_mutex_unlock(&c->mu);
+	if (nsign != NULL)
+		*nsign = ns;
+	if (nvalidate != NULL)
+		*nvalidate = nv;
+	/* the tick works on copies, results are written back */
+	sreq = malloc((ns + 1) * sizeof(*sreq));
+	vreq = malloc((nv + 1) * sizeof(*vreq));
+	if (sreq == NULL || vreq == NULL) {
+		for (size_t i = 0; i < ns; i++)
+			sp[i]->rc = ENOMEM;
+		for (size_t i = 0; i < nv; i++)
+			vp[i]->result = EIO;
+		rc = ENOMEM;
+		goto out;
+	}
+	for (size_t i = 0; i < ns; i++)
+		sreq[i] = *sp[i];
+	for (size_t i = 0; i < nv; i++)
+		vreq[i] = *vp[i];
+	rc = tick(sreq, ns, vreq, nv, c->nthreads);
+	for (size_t i = 0; i < ns; i++)
+		sp[i]->rc = sreq[i].rc;
+	for (size_t i = 0; i < nv; i++)
+		vp[i]->result = vreq[i].result;
+out:
+	free(sreq);
+	free(vreq);
+	free(sp);
+	free(vp);
+	return rc;
+}

@@ -15,9 +15,12 @@
 #include "../../include/net2/hash.h"
 #include "../../include/net2/sign.h"
 #include "../../include/net2/signature.h"
+#include "../../include/net2/signed_carver.h"
 
 #include <errno.h>
+#include <pthread.h>
 #include <stdio.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -247,6 +250,147 @@ test_signatures(struct net2_sign_ctx *priv, struct net2_sign_ctx *pub,
 	free(buf);
 }
 
+/*
+ * Part 3: the signed carver's signature step batched per tick
+ * (net2/signed_carver.h) at BASELINE configs[0]'s shape, 4096 x 1 KiB
+ * payloads: carvers with two sign contexts each (src/signed_carver.c:
+ * 407-432), added from four threads, one tick; then the combiner checks
+ * (:265-338) of every signature, with tampered payloads, an unknown hash
+ * name and a wrong sign algorithm among them, in one more tick.
+ */
+struct adder {
+	struct net2_sc_collector	*c;
+	struct net2_sc_sign_req		*reqs;
+	size_t				 lo, hi;
+};
+
+static void *
+add_some(void *arg)
+{
+	struct adder *a = arg;
+
+	for (size_t i = a->lo; i < a->hi; i++)
+		CHECK(net2_sc_collector_add_sign(a->c, &a->reqs[i]) == 0);
+	return NULL;
+}
+
+static double
+now_s(void)
+{
+	struct timespec ts;
+
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static void
+test_carver_tick(struct net2_sign_ctx *priv, struct net2_sign_ctx *pub,
+    EVP_PKEY *refpub)
+{
+	enum { N = 4096, L = 1024, NS = 2 };
+	uint8_t *buf = malloc((size_t)N * L), dig[64];
+	struct iovec *iov = calloc(2 * N, sizeof(*iov));
+	struct net2_sc_sign_req *reqs = calloc(N, sizeof(*reqs));
+	struct net2_signature *sigs = calloc((size_t)N * NS, sizeof(*sigs));
+	struct net2_sc_validate_req *vr = calloc((size_t)N * NS, sizeof(*vr));
+	struct net2_sign_ctx *ctxs[NS] = { priv, net2_signctx_clone(priv) };
+	struct net2_sc_collector *c = net2_sc_collector_new(8);
+	struct adder ad[4];
+	pthread_t tid[4];
+	size_t ns = 0, nv = 0;
+	double t0, t_sign, t_val;
+	int bad = 0;
+
+	CHECK(c != NULL && ctxs[1] != NULL);
+	for (size_t i = 0; i < (size_t)N * L; i++)
+		buf[i] = rnd8();
+	for (int i = 0; i < N; i++) {
+		/* most payloads one segment, every 5th split in two */
+		iov[2 * i].iov_base = buf + (size_t)i * L;
+		iov[2 * i].iov_len = i % 5 ? L : 300;
+		iov[2 * i + 1].iov_base = buf + (size_t)i * L + 300;
+		iov[2 * i + 1].iov_len = L - 300;
+		reqs[i].payload = &iov[2 * i];
+		reqs[i].iovcnt = i % 5 ? 1 : 2;
+		reqs[i].hash_alg = i % 3 ? 3 : 1;	/* SHA512, some SHA256 */
+		reqs[i].num_signatures = NS;
+		reqs[i].signatures = ctxs;
+		reqs[i].out = &sigs[(size_t)i * NS];
+	}
+	reqs[N - 1].hash_alg = 4;	/* keyed row: not a sighash -> EINVAL */
+	for (int t = 0; t < 4; t++) {
+		ad[t] = (struct adder){ c, reqs, (size_t)N * t / 4,
+		    (size_t)N * (t + 1) / 4 };
+		pthread_create(&tid[t], NULL, add_some, &ad[t]);
+	}
+	for (int t = 0; t < 4; t++)
+		pthread_join(tid[t], NULL);
+	t0 = now_s();
+	CHECK(net2_sc_collector_tick(c, &ns, &nv) == 0);
+	t_sign = now_s() - t0;
+	CHECK(ns == N && nv == 0);
+	CHECK(reqs[N - 1].rc == EINVAL);
+	for (int i = 0; i < N - 1; i++) {
+		CHECK(reqs[i].rc == 0);
+		if (i % 97 != 0)
+			continue;
+		for (int k = 0; k < NS; k++) {
+			struct net2_signature *sg = &sigs[(size_t)i * NS + k];
+			ref_digest(reqs[i].hash_alg, buf + (size_t)i * L, L, dig);
+			CHECK(strcmp(sg->hash_alg,
+			    net2_hash_getname(reqs[i].hash_alg)) == 0);
+			CHECK(ref_verify(refpub, sg->data, sg->datalen, dig,
+			    (size_t)net2_hash_gethashlen(reqs[i].hash_alg)));
+		}
+	}
+	/* checks of every signature, some broken */
+	for (int i = 0; i < N - 1; i++)
+		for (int k = 0; k < NS; k++) {
+			struct net2_sc_validate_req *q = &vr[(size_t)i * NS + k];
+			q->payload = reqs[i].payload;
+			q->iovcnt = reqs[i].iovcnt;
+			q->sig = &sigs[(size_t)i * NS + k];
+			q->sctx = pub;
+			q->result = -1;
+			CHECK(net2_sc_collector_add_validate(c, q) == 0);
+		}
+	for (int i = 10; i < N - 1; i += 211)
+		buf[(size_t)i * L + 700] ^= 0x01;	/* tampered payload */
+	free(sigs[2 * 3].hash_alg);
+	sigs[2 * 3].hash_alg = strdup("MD5");		/* unknown hash */
+	free(sigs[2 * 4 + 1].sign_alg);
+	sigs[2 * 4 + 1].sign_alg = strdup("rsa");	/* wrong sign alg */
+	t0 = now_s();
+	CHECK(net2_sc_collector_tick(c, &ns, &nv) == 0);
+	t_val = now_s() - t0;
+	CHECK(ns == 0 && nv == (size_t)(N - 1) * NS);
+	for (int i = 0; i < N - 1; i++)
+		for (int k = 0; k < NS; k++) {
+			const int r = vr[(size_t)i * NS + k].result;
+			int want = 0;
+			if (i >= 10 && (i - 10) % 211 == 0)
+				want = EINVAL;
+			if ((i == 3 && k == 0) || (i == 4 && k == 1))
+				want = EIO;
+			if (r != want)
+				bad++;
+		}
+	CHECK(bad == 0);
+	/* an empty tick is a no-op */
+	CHECK(net2_sc_collector_tick(c, &ns, &nv) == 0 && ns == 0 && nv == 0);
+	printf("carver tick: %d carvers x %d signatures: sign %.1f ms, "
+	    "validate %.1f ms\n", N, NS, t_sign * 1e3, t_val * 1e3);
+	for (size_t i = 0; i < (size_t)N * NS; i++)
+		net2_signature_deinit(&sigs[i]);
+	net2_sc_collector_free(c);
+	net2_signctx_free(ctxs[1]);
+	free(buf);
+	free(iov);
+	free(reqs);
+	free(sigs);
+	free(vr);
+}
+
 int
 main(int argc, char **argv)
 {
@@ -284,6 +428,7 @@ main(int argc, char **argv)
 		if (!cpu_only) {
 			test_fingerprint(priv, pub);
 			test_signatures(priv, pub, refpub);
+			test_carver_tick(priv, pub, refpub);
 		}
 	}
 	EVP_PKEY_free(refpub);

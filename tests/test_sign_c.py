@@ -26,7 +26,8 @@ def test_sign_library_exports():
     import ilias_net2_amd._lib as L
     L.lib()  # loads libnet2_sha2.so first (same process, one HIP runtime)
     lib = ctypes.CDLL(LIB)
-    for name in _declared("sign.h") | _declared("signature.h") | _declared("wire.h"):
+    for name in (_declared("sign.h") | _declared("signature.h") | _declared("wire.h")
+                 | _declared("signed_carver.h")):
         assert hasattr(lib, name), name
 
 

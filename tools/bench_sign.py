@@ -27,6 +27,25 @@ class Sig(ctypes.Structure):
                 ("data", ctypes.c_void_p), ("datalen", ctypes.c_size_t)]
 
 
+class IOV(ctypes.Structure):
+    _fields_ = [("base", ctypes.c_void_p), ("len", ctypes.c_size_t)]
+
+
+class SignReq(ctypes.Structure):
+    """struct net2_sc_sign_req (include/net2/signed_carver.h)."""
+    _fields_ = [("payload", ctypes.POINTER(IOV)), ("iovcnt", ctypes.c_size_t),
+                ("hash_alg", ctypes.c_int), ("num_signatures", ctypes.c_uint32),
+                ("signatures", ctypes.POINTER(ctypes.c_void_p)),
+                ("out", ctypes.POINTER(Sig)), ("rc", ctypes.c_int)]
+
+
+class ValReq(ctypes.Structure):
+    """struct net2_sc_validate_req (include/net2/signed_carver.h)."""
+    _fields_ = [("payload", ctypes.POINTER(IOV)), ("iovcnt", ctypes.c_size_t),
+                ("sig", ctypes.POINTER(Sig)), ("sctx", ctypes.c_void_p),
+                ("result", ctypes.c_int)]
+
+
 def measure():
     """All stages in one dict (bench.py's extra_configs.c1)."""
     res = stages()
@@ -119,6 +138,51 @@ def stages():
                 "stage": f"net2_signature_validate_batch SHA512+ECDSA-P521, {threads} threads",
                 "payloads_per_s": n / t_v, "ms": t_v * 1e3})
     free_all()
+
+    # the signed carver's signature step, one tick for all 4096 carvers
+    # (src/signed_carver.c:407-432 batched; net2/signed_carver.h)
+    iovs = (IOV * n)()
+    for i in range(n):
+        iovs[i].base = data.ctypes.data + i * length
+        iovs[i].len = length
+    ctxs = (ctypes.c_void_p * 1)(priv.value)
+    reqs = (SignReq * n)()
+    outs = (Sig * n)()
+    for i in range(n):
+        reqs[i].payload = ctypes.pointer(iovs[i])
+        reqs[i].iovcnt = 1
+        reqs[i].hash_alg = 3
+        reqs[i].num_signatures = 1
+        reqs[i].signatures = ctxs
+        reqs[i].out = ctypes.pointer(outs[i])
+    vreqs = (ValReq * n)()
+    for i in range(n):
+        vreqs[i].payload = ctypes.pointer(iovs[i])
+        vreqs[i].iovcnt = 1
+        vreqs[i].sig = ctypes.pointer(outs[i])
+        vreqs[i].sctx = pub.value
+
+    def sign_tick():
+        for i in range(n):
+            S.net2_signature_deinit(ctypes.byref(outs[i]))
+        rc = S.net2_signed_carver_sign_tick(reqs, ctypes.c_size_t(n), threads)
+        assert rc == 0, rc
+
+    def validate_tick():
+        rc = S.net2_signed_combiner_validate_tick(vreqs, ctypes.c_size_t(n), threads)
+        assert rc == 0, rc
+    t_st = timeit(sign_tick, reps=2)
+    assert all(reqs[i].rc == 0 for i in range(n))
+    t_vt = timeit(validate_tick, reps=2)
+    assert all(vreqs[i].result == 0 for i in range(n))
+    res.append({"key": "signed_carver_sign_tick",
+                "stage": f"net2_signed_carver_sign_tick: {n} carvers x 1 SHA512+ECDSA-P521 signature, one tick, {threads} threads",
+                "payloads_per_s": n / t_st, "ms": t_st * 1e3})
+    res.append({"key": "signed_combiner_validate_tick",
+                "stage": f"net2_signed_combiner_validate_tick: {n} checks, one tick, {threads} threads",
+                "payloads_per_s": n / t_vt, "ms": t_vt * 1e3})
+    for i in range(n):
+        S.net2_signature_deinit(ctypes.byref(outs[i]))
     return res
 
 
