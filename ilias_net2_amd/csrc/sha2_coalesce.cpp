@@ -50,6 +50,9 @@ typedef std::chrono::steady_clock clk;
 constexpr int kMaxSlots = 16;
 constexpr size_t kInitialStage = 1u << 20;	/* grows on demand */
 constexpr size_t kMaxJobs = 1u << 16;		/* per batch */
+/* Up to this many jobs a batch runs one wave per job (job_wave_kernel):
+ * ~4 waves per SIMD of the 256 CUs still start at once. */
+constexpr size_t kWaveJobsMax = 1024;
 
 int env_int(const char *name, int dflt, int lo, int hi)
 {
@@ -139,7 +142,8 @@ public:
 	    : nslots_(env_int("NET2_COALESCE_SLOTS", 4, 1, kMaxSlots)),
 	      window_(std::chrono::microseconds(
 		  env_int("NET2_COALESCE_WINDOW_US", 40, 0, 100000))),
-	      zerocopy_(env_int("NET2_COALESCE_ZEROCOPY", 0, 0, 1) != 0)
+	      zerocopy_(env_int("NET2_COALESCE_ZEROCOPY", 0, 0, 1) != 0),
+	      jobmode_(env_int("NET2_COALESCE_JOBMODE", 0, 0, 2))
 	{
 		for (int i = nslots_ - 1; i >= 0; i--)
 			free_.push_back(i);
@@ -158,6 +162,7 @@ private:
 	const int nslots_;
 	const clk::duration window_;
 	const bool zerocopy_;
+	const int jobmode_;	/* 0 auto, 1 wave per job, 2 lane per job */
 	int open_ = -1;
 	std::vector<int> free_;
 	int inflight_ = 0;
@@ -441,6 +446,7 @@ int Coalescer::launch_and_wait(Slot &s, int ordinal, int *hip_err)
 	const size_t n = jobs.size();
 	size_t hdr_off, n256;
 	uint32_t waves, target;
+	int wave;
 	const uint8_t *stage;
 	uint8_t *d_out;
 	uint32_t *d_done;
@@ -485,11 +491,15 @@ int Coalescer::launch_and_wait(Slot &s, int ordinal, int *hip_err)
 		    hdr_off + n * sizeof(Net2Job), hipMemcpyHostToDevice,
 		    s.stream));
 	stage = s.d_stage;
-	waves = (uint32_t)((n256 + 63) / 64 + (n - n256 + 63) / 64);
+	/* few jobs: a wave each (lower latency, the GPU is idle anyway);
+	 * many: a lane each */
+	wave = jobmode_ == 1 || (jobmode_ == 0 && n <= kWaveJobsMax);
+	waves = wave ? (uint32_t)n :
+	    (uint32_t)((n256 + 63) / 64 + (n - n256 + 63) / 64);
 	target = s.done_base + waves;
 	CO_TRY(net2_launch_jobs(stage,
 	    reinterpret_cast<const Net2Job *>(stage + hdr_off), (uint32_t)n256,
-	    (uint32_t)(n - n256), d_out, d_done, s.stream));
+	    (uint32_t)(n - n256), d_out, d_done, wave, s.stream));
 	CO_TRY(hipEventRecord(s.ev, s.stream));
 	{
 		/*

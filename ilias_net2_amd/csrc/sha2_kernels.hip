@@ -1027,6 +1027,174 @@ __global__ __launch_bounds__(64) void job_kernel(const uint8_t *__restrict__ sta
 		    __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+/*
+ * Latency form of job_kernel: one wave per job, for batches small enough
+ * that the GPU is otherwise idle (a lone caller, a few threads).  A lane of
+ * job_kernel runs message expansion and rounds of every block one after the
+ * other; here the 64 lanes first expand up to 64 blocks of the job at once
+ * (block b's K[t] + W[t] by lane b, into LDS -- the schedule of a block
+ * depends only on its message words, not on the chaining state), then the
+ * wave runs only the rounds, block after block, reading K + W from LDS.
+ * About a third of a compression's instructions leave the serial chain.
+ */
+#define NET2_JOB_ROW256 65	/* dwords per LDS row: odd, so the 64 lanes'
+				 * row writes fall in distinct banks */
+#define NET2_JOB_ROW512 81	/* qwords per row */
+
+template <int T>
+struct Sched256 {
+	__device__ __forceinline__ static void run(uint32_t (&w)[16],
+	    uint32_t *row)
+	{
+		const uint32_t wt = T < 16 ? w[T & 15] : expand256<T, false>(w);
+		row[T] = wt + K256[T];
+		Sched256<T + 1>::run(w, row);
+	}
+};
+template <>
+struct Sched256<64> {
+	__device__ __forceinline__ static void run(uint32_t (&)[16], uint32_t *) {}
+};
+
+template <int T>
+struct Sched512 {
+	__device__ __forceinline__ static void run(uint64_t (&w)[16],
+	    uint64_t *row, const lds_k64 *kb)
+	{
+		const uint64_t wt = T < 16 ? w[T & 15] : expand512<T>(w);
+		row[T] = addk512<T>(wt, kb);
+		Sched512<T + 1>::run(w, row, kb);
+	}
+};
+template <>
+struct Sched512<80> {
+	__device__ __forceinline__ static void run(uint64_t (&)[16], uint64_t *,
+	    const lds_k64 *) {}
+};
+
+template <int T>
+struct RowRounds512 {
+	__device__ __forceinline__ static void run(uint64_t (&s)[8],
+	    const uint64_t *row)
+	{
+		round512<T>(s, row[T]);
+		RowRounds512<T + 1>::run(s, row);
+	}
+};
+template <>
+struct RowRounds512<80> {
+	__device__ __forceinline__ static void run(uint64_t (&)[8],
+	    const uint64_t *) {}
+};
+
+/* Expand block `blk` (big-endian words) into its K + W row. */
+template <class H>
+__device__ __forceinline__ void sched_row(uint32_t (&blk)[H::NW32],
+    typename H::word *row)
+{
+	if constexpr (sizeof(typename H::word) == 4) {
+		Sched256<0>::run(blk, row);
+	} else {
+		uint64_t w[16];
+#pragma unroll
+		for (int i = 0; i < 16; i++)
+			w[i] = mk64(blk[2 * i + 1], blk[2 * i]);
+		Sched512<0>::run(w, row, k512_base());
+	}
+}
+
+/* The rounds of one block from its K + W row (all lanes, same state). */
+template <class H>
+__device__ __forceinline__ void rounds_row(typename H::State &st,
+    const typename H::word *row)
+{
+	if constexpr (sizeof(typename H::word) == 4) {
+		compress256_kw<H::ASM>(st, row);
+	} else {
+		uint64_t s[8];
+#pragma unroll
+		for (int i = 0; i < 8; i++)
+			s[i] = st[i];
+		RowRounds512<0>::run(s, row);
+#pragma unroll
+		for (int i = 0; i < 8; i++)
+			st[i] += s[i];
+	}
+}
+
+template <class H>
+__global__ __launch_bounds__(64) void job_wave_kernel(const uint8_t *__restrict__ stage,
+    const Net2Job *__restrict__ jobs, uint8_t *__restrict__ out,
+    uint32_t *done)
+{
+	constexpr int NW32 = H::NW32;
+	typedef typename H::word W;
+	constexpr int ROW = sizeof(W) == 4 ? NET2_JOB_ROW256 : NET2_JOB_ROW512;
+	__shared__ W rows[64 * ROW];
+	if (sizeof(W) == 8)
+		k512_lds_fill();
+	const uint32_t lane = threadIdx.x;
+	const Net2Job jb = jobs[blockIdx.x];
+	const int is384 = (jb.flags & 0xffu) == NET2_ALG_SHA384;
+	typename H::State st;
+	if (jb.flags & NET2_JOB_STATE) {
+		const W *s0 = reinterpret_cast<const W *>(stage + jb.aux);
+#pragma unroll
+		for (int i = 0; i < 8; i++)
+			st[i] = s0[i];
+	} else {
+		H::init(st, is384);
+	}
+	const uint8_t *p = stage + jb.data;
+	for (uint32_t c0 = 0; c0 < jb.nblk; c0 += 64) {
+		const uint32_t nb = min(64u, jb.nblk - c0);
+		if (lane < nb) {
+			const uint8_t *bp = p + (size_t)(c0 + lane) * H::BLOCK;
+			Raw<NW32> r;
+			issue_block<NW32, AMODE_A16>(bp, r);
+			uint32_t w[NW32];
+			finish_block<NW32, AMODE_A16>(bp, r, w);
+			sched_row<H>(w, rows + lane * ROW);
+		}
+		__syncthreads();
+		for (uint32_t b = 0; b < nb; b++)
+			rounds_row<H>(st, rows + b * ROW);
+		__syncthreads();
+	}
+	if (jb.flags & NET2_JOB_HMAC) {
+		uint32_t w[NW32];
+#pragma unroll
+		for (int i = 0; i < NW32; i++)
+			w[i] = 0;
+		const int dw = digest_words<H>(st, is384, w);
+#pragma unroll
+		for (int i = 12; i < 16; i++)
+			if (i >= dw)
+				w[i] = 0;
+		w[dw] = 0x80000000u;
+		const uint64_t obits = (uint64_t)(H::BLOCK + 4 * dw) << 3;
+		w[NW32 - 2] = (uint32_t)(obits >> 32);
+		w[NW32 - 1] = (uint32_t)obits;
+		H::init(st, is384);
+		Raw<NW32> r;
+		issue_block<NW32, AMODE_A16>(stage + jb.aux, r);
+		uint32_t kb[NW32];
+		finish_block<NW32, AMODE_A16>(stage + jb.aux, r, kb);
+		H::compress(st, kb);
+		H::compress(st, w);
+	}
+	if (lane == 0) {
+		W *o = reinterpret_cast<W *>(out + 64 * (size_t)blockIdx.x);
+#pragma unroll
+		for (int i = 0; i < 8; i++)
+			o[i] = st[i];
+	}
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+	if (lane == 0)
+		__hip_atomic_fetch_add(done, 1u, __ATOMIC_RELEASE,
+		    __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 /* ---- packet-header IV derivation (types/packet.n2t:100-158) ---------------- */
 
 /*
@@ -1642,9 +1810,19 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 	return hipGetLastError();
 }
 hipError_t net2_launch_jobs(const uint8_t *stage, const Net2Job *jobs,
-    uint32_t n256, uint32_t n512, uint8_t *out, uint32_t *done,
+    uint32_t n256, uint32_t n512, uint8_t *out, uint32_t *done, int wave,
     hipStream_t s)
 {
+	if (wave) {
+		/* one 64-lane workgroup (one wave) per job */
+		if (n256 > 0)
+			job_wave_kernel<Sha256><<<n256, 64, 0, s>>>(stage, jobs,
+			    out, done);
+		if (n512 > 0)
+			job_wave_kernel<Sha512><<<n512, 64, 0, s>>>(stage,
+			    jobs + n256, out + 64 * (size_t)n256, done);
+		return hipGetLastError();
+	}
 	/* 64-lane workgroups: a few jobs spread over as many CUs as waves */
 	if (n256 > 0)
 		job_kernel<Sha256><<<(n256 + 63) / 64, 64, 0, s>>>(stage, jobs,

@@ -69,9 +69,14 @@ struct Net2Job {
 	uint32_t nblk;
 	uint32_t flags;		/* alg | NET2_JOB_* */
 };
-/* jobs [0, n256) are SHA-256, [n256, n256 + n512) SHA-384/512. */
+/*
+ * jobs [0, n256) are SHA-256, [n256, n256 + n512) SHA-384/512.  wave == 0:
+ * one lane per job (throughput form, a wave per 64 jobs of a family);
+ * wave != 0: one wave per job (latency form: the lanes expand the job's
+ * blocks in parallel, the wave runs the rounds).
+ */
 hipError_t net2_launch_jobs(const uint8_t *stage, const Net2Job *jobs,
-    uint32_t n256, uint32_t n512, uint8_t *out, uint32_t *done,
+    uint32_t n256, uint32_t n512, uint8_t *out, uint32_t *done, int wave,
     hipStream_t s);
 
 /*

@@ -234,3 +234,49 @@ def test_coalesced_batches_form(L, oracle_mod):
     assert not bad
     # 1,600 calls; serialised they would take 1600 * single
     assert el < 1600 * single / 2, (el, single)
+
+
+_FORM_CHECK = r'''
+import sys, ctypes
+sys.path.insert(0, ".")
+sys.path.insert(0, "tests")
+import numpy as np
+import torch  # noqa: F401  (one HIP runtime: torch first)
+from ilias_net2_amd import hash as h, _lib
+from oracle import oracle
+L = _lib.lib()
+rng = np.random.default_rng(9)
+bad = 0
+for n in (0, 1, 63, 64, 119, 128, 1024, 5000, 70000):
+    m = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    for alg in (1, 2, 3):
+        bad += h.hashbuf(alg, b"", m) != oracle.digest(alg, m)
+        key = bytes(range(7, 7 + {1: 32, 2: 48, 3: 64}[alg]))
+        bad += h.hashbuf(alg + 3, key, m) != oracle.hmac(alg + 3, key, m)
+        ctx = ctypes.create_string_buffer(208)
+        L.net2_sha2_ctx_init(alg, ctx)
+        for a in range(0, n, 999):
+            seg = m[a:a + 999]
+            L.net2_sha2_ctx_update(alg, ctx, seg, len(seg))
+        d = ctypes.create_string_buffer(64)
+        L.net2_sha2_ctx_final(alg, d, ctx)
+        bad += d.raw[:{1: 32, 2: 48, 3: 64}[alg]] != oracle.digest(alg, m)
+print("BAD", bad)
+'''
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_wave_and_lane_job_forms(L, mode):
+    """Both kernels behind the coalescer -- one wave per job (the latency
+    form, used up to 1,024 jobs a batch) and one lane per job -- forced in a
+    fresh process each (NET2_COALESCE_JOBMODE), messages up to 70,000 bytes
+    (more than 64 blocks: the wave form's chunk loop)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, NET2_COALESCE_JOBMODE=mode)
+    r = subprocess.run([sys.executable, "-c", _FORM_CHECK], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "BAD 0" in r.stdout, r.stdout + r.stderr
