@@ -50,9 +50,16 @@ typedef std::chrono::steady_clock clk;
 constexpr int kMaxSlots = 16;
 constexpr size_t kInitialStage = 1u << 20;	/* grows on demand */
 constexpr size_t kMaxJobs = 1u << 16;		/* per batch */
-/* Up to this many jobs a batch runs one wave per job (job_wave_kernel):
- * ~4 waves per SIMD of the 256 CUs still start at once. */
-constexpr size_t kWaveJobsMax = 1024;
+/*
+ * Up to this many jobs a batch runs one wave per job (job_wave_kernel, the
+ * latency form); larger batches one lane per job.  Measured with
+ * tools/coalesce_bench.c, 1 KiB messages (profiles/round2/coalesce_jm*):
+ * the wave form cuts a lone call from 82 to 50 us (SHA-512) and 64 to
+ * 55 us (SHA-256) and wins at 8 threads; at 64 threads, where batches
+ * hold tens of jobs, the lane form keeps up equally (SHA-512) or better
+ * (SHA-256: 433 k vs 349 k calls/s).
+ */
+constexpr size_t kWaveJobsMax = 16;
 
 int env_int(const char *name, int dflt, int lo, int hi)
 {
