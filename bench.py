@@ -498,8 +498,8 @@ def main():
         line["roofline_valu"] = valu
     gpu["sclk_mhz_during_timed_steps"] = r["sclk_during_mhz"]
     line["gpu"] = gpu
-    if ws == 1 and name == "c2" and not args.no_extras:
-        line["extra_configs"] = extra_configs(args, dev, probe)
+    if name == "c2" and not args.no_extras:
+        line["extra_configs"] = extra_configs(args, dev, probe, ws, rank)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and name in ("c2", "c3", "c4"):
         line["cpu_baseline"] = cpu_baseline(cfg)
     if rank == 0:
@@ -509,12 +509,18 @@ def main():
     return None
 
 
-def extra_configs(args, dev, probe):
-    """The other BASELINE.json configs, timed in the same invocation on the
-    same GPU: C3 (mixed lengths, binned) and C4 (SHA-512) device-resident
-    with their rooflines; the end-to-end host-memory rate per GPU (C5's
-    per-GPU shape); C1 (4096 x 1 KiB signed payloads)."""
+def extra_configs(args, dev, probe, ws=1, rank=0):
+    """The other BASELINE.json configs, timed in the same invocation: at
+    N=1, C3 (mixed lengths, binned) and C4 (SHA-512) device-resident with
+    their rooflines, C1 (4096 x 1 KiB signed payloads) and the end-to-end
+    host-memory rate; at N>1 the end-to-end rate over all ranks -- C5,
+    1 M x 1 KiB per GPU from pinned host memory through every GPU at once
+    (8 M at N=8), the max over ranks of the per-step time."""
     out = {}
+    if ws > 1:
+        out["e2e"] = e2e_rate(steps=10, warmup=3, ws=ws, dev=dev,
+                              dist_backend=args.dist_backend)
+        return out
     for name in ("c3", "c4"):
         r = time_device_config(name, dev, args.steps, min(args.warmup, 10),
                                200.0, clock_probe=probe)
@@ -532,10 +538,13 @@ def extra_configs(args, dev, probe):
     return out
 
 
-def e2e_rate(steps, warmup, n=1 << 20, length=1024):
-    """C5's per-GPU shape: 1 M x 1 KiB from pinned host memory -> this GPU ->
-    digests back to pinned host memory, through net2_sha2_batch."""
+def e2e_rate(steps, warmup, n=1 << 20, length=1024, ws=1, dev=None,
+             dist_backend="nccl"):
+    """C5's shape: 1 M x 1 KiB per GPU from pinned host memory -> the GPU ->
+    digests back to pinned host memory, through net2_sha2_batch (each rank
+    on its own GPU, max_devices 1); timed between barriers, max over ranks."""
     import torch
+    import torch.distributed as dist
     from ilias_net2_amd import _lib
     host = torch.randint(0, 256, (n * length,), dtype=torch.uint8).pin_memory()
     outp = torch.empty((n, 32), dtype=torch.uint8).pin_memory()
@@ -546,17 +555,27 @@ def e2e_rate(steps, warmup, n=1 << 20, length=1024):
                                      length, n, outp.data_ptr(), 1))
     for _ in range(warmup):
         step()
+    if ws > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
+    if ws > 1:
+        dist.barrier()
     ms = (time.perf_counter() - t0) * 1e3 / steps
+    if ws > 1:
+        t = torch.tensor([ms], dtype=torch.float64,
+                         device=dev if dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t[0])
     del host, outp
     return {"metric": "SHA-256 digests/s, 1 KiB packets from pinned host memory, "
-                      "end to end (H2D + kernel + D2H), one GPU",
-            "value": round(n / (ms / 1e3), 1), "unit": "digests/s", "steps": steps,
-            "ms_per_step": round(ms, 3),
-            "workload": "1M x 1 KiB per GPU, host -> GPU -> host via net2_sha2_batch (BASELINE configs[4] per-GPU shape)",
-            "h2d_GBps": round(n * length / (ms / 1e3) / 1e9, 2)}
+                      f"end to end (H2D + kernel + D2H), {ws} GPU(s)",
+            "value": round(n * ws / (ms / 1e3), 1), "unit": "digests/s", "steps": steps,
+            "n_gpus": ws, "ms_per_step": round(ms, 3),
+            "workload": f"{ws} x 1M x 1 KiB, host -> GPU -> host via net2_sha2_batch, "
+                        "one rank per GPU (BASELINE configs[4] at N=8)",
+            "h2d_GBps_per_gpu": round(n * length / (ms / 1e3) / 1e9, 2)}
 
 
 def run_c1():
@@ -575,17 +594,10 @@ def run_e2e(args, ws, rank, dev):
     through net2_sha2_batch on this rank's device (PCIe-inclusive rate)."""
     import torch
     import torch.distributed as dist
-    if ws > 1:
-        dist.barrier()
     t0 = time.perf_counter()
-    r = e2e_rate(args.steps, args.warmup)
+    r = e2e_rate(args.steps, args.warmup, ws=ws, dev=dev,
+                 dist_backend=args.dist_backend)
     el = time.perf_counter() - t0
-    if ws > 1:
-        t = torch.tensor([r["ms_per_step"]], dtype=torch.float64,
-                         device=dev if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        r["ms_per_step"] = float(t[0])
-        r["value"] = round((1 << 20) * ws / (r["ms_per_step"] / 1e3), 1)
     r.update({"n_gpus": ws, "warmup": args.warmup, "higher_is_better": True,
               "scaling": "weak", "vs_baseline": None, "dtype": "u32",
               "data": "synthetic random bytes in pinned host memory",
