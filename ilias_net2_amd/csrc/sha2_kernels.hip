@@ -1569,6 +1569,85 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(
 	}
 }
 
+/*
+ * Tile-local binning (NET2_BIN_TILESORT, the default): one launch, no
+ * global histogram.  Workgroup t counting-sorts its own tile of
+ * NET2_BIN_TILE_SORT packets by descending block count in LDS and writes
+ * the tile's visiting order to perm[t * TILE ...].  Waves of the hash
+ * kernel then take 64 consecutive entries of one tile: length-uniform
+ * except the few waves that straddle a bin boundary inside a tile (with
+ * 8,192-packet tiles, 2 of 128 waves for a {64, 512, 1500} mix).  Against
+ * the global order of bin_count + bin_scatter this drops the memset, one
+ * kernel and two launch gaps per batch, and the waves of a tile read their
+ * descriptors from one contiguous range.
+ */
+#ifndef NET2_BIN_TILESORT
+#define NET2_BIN_TILESORT 1
+#endif
+#ifndef NET2_BIN_SORT_ITEMS
+#define NET2_BIN_SORT_ITEMS 32
+#endif
+#define NET2_BIN_TILE_SORT (256 * NET2_BIN_SORT_ITEMS)
+
+__global__ __launch_bounds__(256) void bin_tile_kernel(
+    const uint32_t *__restrict__ lens, uint64_t n, int blk_shift,
+    int lenbytes, uint32_t *__restrict__ perm)
+{
+	__shared__ uint32_t cnt[NET2_SHA2_NBINS];
+	__shared__ uint32_t wsum[4];
+	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
+		cnt[b] = 0;
+	__syncthreads();
+	const uint64_t t0 = (uint64_t)blockIdx.x * NET2_BIN_TILE_SORT;
+	uint32_t bin[NET2_BIN_SORT_ITEMS], rank[NET2_BIN_SORT_ITEMS];
+#pragma unroll
+	for (int k = 0; k < NET2_BIN_SORT_ITEMS; k++) {
+		const uint64_t i = t0 + (uint64_t)k * 256 + threadIdx.x;
+		bin[k] = i < n ? lens[i] : 0u;
+	}
+#pragma unroll
+	for (int k = 0; k < NET2_BIN_SORT_ITEMS; k++) {
+		const bool live = t0 + (uint64_t)k * 256 + threadIdx.x < n;
+		bin[k] = live ? bin_of(bin[k], blk_shift, lenbytes,
+		    NET2_SHA2_NBINS) : 0;
+		rank[k] = live ? atomicAdd(&cnt[bin[k]], 1u) : 0u;
+	}
+	__syncthreads();
+	/* exclusive scan of the tile histogram: 8 bins per thread, a shuffle
+	 * scan per wave, the four wave totals */
+	constexpr int PER = NET2_SHA2_NBINS / 256;
+	const int lane = (int)__lane_id(), wave = (int)(threadIdx.x / 64);
+	uint32_t v[PER], sum = 0;
+#pragma unroll
+	for (int j = 0; j < PER; j++) {
+		v[j] = sum;
+		sum += cnt[threadIdx.x * PER + j];
+	}
+	uint32_t x = sum;
+#pragma unroll
+	for (int off = 1; off < 64; off <<= 1) {
+		const uint32_t y = __shfl_up(x, off);
+		if (lane >= off)
+			x += y;
+	}
+	if (lane == 63)
+		wsum[wave] = x;
+	__syncthreads();
+	uint32_t base = x - sum;
+	for (int w = 0; w < wave; w++)
+		base += wsum[w];
+#pragma unroll
+	for (int j = 0; j < PER; j++)
+		cnt[threadIdx.x * PER + j] = base + v[j];
+	__syncthreads();
+#pragma unroll
+	for (int k = 0; k < NET2_BIN_SORT_ITEMS; k++) {
+		const uint64_t i = t0 + (uint64_t)k * 256 + threadIdx.x;
+		if (i < n)
+			perm[t0 + cnt[bin[k]] + rank[k]] = (uint32_t)i;
+	}
+}
+
 /* ---- host-side constant pad schedule ---------------------------------- */
 
 static inline uint32_t h_ror32(uint32_t x, int n)
@@ -1678,6 +1757,13 @@ hipError_t net2_bin_order(int alg, const uint32_t *lens, uint64_t n,
 	uint32_t *hist = ws;
 	uint32_t *cursor = ws + NET2_SHA2_NBINS;
 	uint32_t *perm = ws + 2 * NET2_SHA2_NBINS;
+	if (NET2_BIN_TILESORT) {
+		const unsigned g = (unsigned)((n + NET2_BIN_TILE_SORT - 1) /
+		    NET2_BIN_TILE_SORT);
+		bin_tile_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift, lenbytes,
+		    perm);
+		return hipGetLastError();
+	}
 	/* fused: cursor holds per-bin claim counters, zeroed with hist */
 	hipError_t e = hipMemsetAsync(hist, 0, (NET2_BIN_FUSED ? 2 : 1) *
 	    NET2_SHA2_NBINS * sizeof(uint32_t), s);
