@@ -1570,19 +1570,19 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(
 }
 
 /*
- * Tile-local binning (NET2_BIN_TILESORT, the default): one launch, no
- * global histogram.  Workgroup t counting-sorts its own tile of
- * NET2_BIN_TILE_SORT packets by descending block count in LDS and writes
- * the tile's visiting order to perm[t * TILE ...].  Waves of the hash
- * kernel then take 64 consecutive entries of one tile: length-uniform
- * except the few waves that straddle a bin boundary inside a tile (with
- * 8,192-packet tiles, 2 of 128 waves for a {64, 512, 1500} mix).  Against
- * the global order of bin_count + bin_scatter this drops the memset, one
- * kernel and two launch gaps per batch, and the waves of a tile read their
- * descriptors from one contiguous range.
+ * Tile-local binning (NET2_BIN_TILESORT=1; measured and NOT the default):
+ * one launch, no global histogram -- workgroup t counting-sorts its own
+ * tile of NET2_BIN_TILE_SORT packets by descending block count in LDS.
+ * Waves stay length-uniform, the binning itself takes 10 us instead of
+ * ~16 us plus a memset and a launch gap, yet the hash kernel runs 2x
+ * slower (C3: 904 us against 442 us, profiles/round2/binning_tile_ab.txt):
+ * the global order is also a longest-first schedule.  A wave of 1,500-byte
+ * packets lives ~170 us at 3 waves per SIMD; dispatched first, the long
+ * waves finish while short ones fill in behind them, whereas tile order
+ * keeps starting long waves until the very end of the grid.
  */
 #ifndef NET2_BIN_TILESORT
-#define NET2_BIN_TILESORT 1
+#define NET2_BIN_TILESORT 0
 #endif
 #ifndef NET2_BIN_SORT_ITEMS
 #define NET2_BIN_SORT_ITEMS 32
