@@ -15,8 +15,10 @@ and error behaviour:
   ``std::invalid_argument`` of the C++ code), and a keyed hash needs a key of
   exactly ``keylen`` bytes (hash-openssl.cc:101).
 
-Every digest is computed on the GPU through ``net2_hashctx_hashiov``; with no
-usable device the calls raise ``Net2Error(ENODEV)``.
+Every digest is computed on the GPU: ``run``/``hashbuf`` through
+``net2_hashctx_hashiov`` (one coalesced request), ``instantiate`` through the
+streaming SHA2_CTX calls of net2/sha2.h; with no usable device the calls raise
+``Net2Error(ENODEV)``.
 """
 from __future__ import annotations
 
@@ -81,27 +83,54 @@ def hashbuf(alg: int, key: Bytes, data: Union[Bytes, Iterable[Bytes]]) -> bytes:
 
 
 class HashCtx:
-    """ilias::hash_ctx: buffers update() segments, digests on final()."""
+    """ilias::hash_ctx (include/ilias/net2/hash.h:31-45), streaming: a
+    SHA2_CTX of net2/sha2.h (src/sha2.c's context) whose compressions run on
+    the GPU as update() completes blocks; keyed rows keep an inner context
+    primed with K' ^ ipad and run the outer hash at final() (RFC 2104), as
+    the C++ backend does (ilias_net2_amd/csrc/cxx/hash_mi355x.cc)."""
+
+    _SHA_ROW = {1: 1, 2: 2, 3: 3, 4: 1, 5: 2, 6: 3}
 
     def __init__(self, factory: "HashCtxFactory", key: bytes):
         self.name = factory.name
         self.hashlen = factory.hashlen
         self.keylen = factory.keylen
-        self._alg = factory.alg
-        self._key = key
-        self._segs: List[bytes] = []
+        self._sha = self._SHA_ROW[factory.alg]
+        self._blk = 64 if self._sha == 1 else 128
+        self._ctx = ctypes.create_string_buffer(208)
+        self._kpad = bytes(key) + b"\0" * (self._blk - len(key))
         self._done = False
+        L = _lib.lib()
+        _lib.check(L.net2_sha2_ctx_init(self._sha, self._ctx), "SHA2 init")
+        if self.keylen:
+            ipad = bytes(b ^ 0x36 for b in self._kpad)
+            self._update(ipad)
+
+    def _update(self, b: bytes) -> None:
+        buf = ctypes.create_string_buffer(b, max(len(b), 1))
+        _lib.check(_lib.lib().net2_sha2_ctx_update(self._sha, self._ctx, buf,
+                                                   len(b)), "SHA2 update")
 
     def update(self, data: Bytes) -> None:
         if self._done:
             raise RuntimeError("hash_ctx already finalized")
-        self._segs.append(bytes(data))
+        self._update(bytes(data))
 
     def final(self) -> bytes:
         if self._done:
             raise RuntimeError("hash_ctx already finalized")
         self._done = True
-        return hashbuf(self._alg, self._key, self._segs)
+        L = _lib.lib()
+        out = ctypes.create_string_buffer(64)
+        _lib.check(L.net2_sha2_ctx_final(self._sha, out, self._ctx), "SHA2 final")
+        if not self.keylen:
+            return out.raw[:self.hashlen]
+        inner = out.raw[:self.hashlen]
+        _lib.check(L.net2_sha2_ctx_init(self._sha, self._ctx), "HMAC final")
+        self._update(bytes(b ^ 0x5C for b in self._kpad))
+        self._update(inner)
+        _lib.check(L.net2_sha2_ctx_final(self._sha, out, self._ctx), "HMAC final")
+        return out.raw[:self.hashlen]
 
 
 class HashCtxFactory:
