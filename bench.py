@@ -166,20 +166,27 @@ def cpu_baseline(cfg):
     n = cfg["n"]
     if cfg["kind"] == "fixed":
         data = synth.fixed_batch(2, n, cfg["length"])
-        run = lambda t, m=n: oracle.batch(alg, data, stride=cfg["length"],  # noqa: E731
-                                          length=cfg["length"], n=m, nthreads=t)
+        run = lambda t, m=n, u=False: oracle.batch(  # noqa: E731
+            alg, data, stride=cfg["length"], length=cfg["length"], n=m,
+            nthreads=t, unrolled=u)
     else:
         lens = synth.mixed_lengths(3, n)
         data, offs = synth.packed(4, lens)
-        run = lambda t, m=n: oracle.batch(alg, data, offsets=offs[:m],  # noqa: E731
-                                          lens=lens[:m], nthreads=t)
+        run = lambda t, m=n, u=False: oracle.batch(  # noqa: E731
+            alg, data, offsets=offs[:m], lens=lens[:m], nthreads=t, unrolled=u)
+    # both transforms of src/sha2.c: rolled (:374-445, the default build)
+    # and unrolled (:316-370, SHA2_UNROLL_TRANSFORM)
     t_share = _time_oracle(run, share)
     t_all = _time_oracle(run, allc, reps=5)
+    t_share_u = _time_oracle(lambda t: run(t, n, True), share)
     # one thread, on the first n/16 packets (same shape)
     n1 = max(1, n // 16)
     t0 = time.perf_counter()
     run(1, n1)
     single = n1 / (time.perf_counter() - t0)
+    t0 = time.perf_counter()
+    run(1, n1, True)
+    single_u = n1 / (time.perf_counter() - t0)
     what = cfg["workload"].split(" packets")[0]
     topo = _cpu_topology()
     # The headline is the best measured rate.  On the GPU boxes of this pool
@@ -187,22 +194,30 @@ def cpu_baseline(cfg):
     # grants 16 CPUs of time (cpu.max "1600000 100000"), so a thread per
     # host CPU runs no faster than 16; the whole-node rate is then
     # extrapolated, and labelled so, from the one-thread rate.
-    best_t, best_threads = min((t_share, share), (t_all, allc))
+    best_t, best_threads, best_form = min((t_share, share, "rolled"),
+                                          (t_all, allc, "rolled"),
+                                          (t_share_u, share, "unrolled"))
+    form_ref = {"rolled": "src/sha2.c:374-445", "unrolled": "src/sha2.c:316-370"}
     phys = topo.get("physical_cores")
     return {"value": n / best_t, "unit": "digests/s", "cores": best_threads,
             "kind": "port",
             "sample": (f"the full {what} packet batch from host memory, "
-                       f"oracle/sha2_oracle.c (-O3, rolled transform like "
-                       f"src/sha2.c:374-445) on {best_threads} pthreads, best "
-                       f"of 3-5 after a warm-up (faster of: the 16-thread "
-                       f"per-GPU share, one thread per usable host CPU)"),
+                       f"oracle/sha2_oracle.c (-O3, {best_form} transform like "
+                       f"{form_ref[best_form]}) on {best_threads} pthreads, best "
+                       f"of 3-5 after a warm-up (fastest of: the 16-thread "
+                       f"per-GPU share, one thread per usable host CPU, the "
+                       f"unrolled transform on the 16-thread share)"),
             "per_gpu_share": {"value": n / t_share, "threads": share},
             "all_host_cpus": {"value": n / t_all, "threads": allc,
                               "note": "one thread per CPU in the affinity mask; "
                                       "bounded by cgroup_cpu_quota when one is set"},
+            "unrolled_transform": {"value": n / t_share_u, "threads": share,
+                                   "single_thread_value": single_u,
+                                   "form": "SHA2_UNROLL_TRANSFORM, " + form_ref["unrolled"]},
             "whole_node_extrapolated": (
-                {"value": single * phys, "basis": f"single_thread_value x {phys} physical cores "
-                                                  "(an estimate, not a measurement; SMT not credited)"}
+                {"value": max(single, single_u) * phys,
+                 "basis": f"best single_thread_value x {phys} physical cores "
+                          "(an estimate, not a measurement; SMT not credited)"}
                 if phys else None),
             "single_thread_value": single,
             "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
@@ -339,7 +354,16 @@ def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
         a.record(stream)
         step()
         b.record(stream)
-    clk = clock_probe() if clock_probe else None  # while the steps run
+    # shader clock while the queued steps run: sampled every ~2 ms until the
+    # last step's event completes (host-side reads, off the GPU's path)
+    samples = []
+    while clock_probe is not None:
+        c = clock_probe()
+        if c:
+            samples.append(c)
+        if ev[-1][1].query() or not c:
+            break
+        time.sleep(0.002)
     torch.cuda.synchronize(dev)
     if ws > 1:
         dist.barrier()
@@ -357,13 +381,15 @@ def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
         (12 * n if cfg["kind"] in ("mixed", "dgram_verify") else 0)
     res = {"n": n, "dlen": dlen, "payload": inp["payload"], "elapsed": elapsed,
            "ms_per_step": elapsed * 1e3 / steps, "launch_ms": launch_ms,
-           "per_launch_bytes": per_launch, "sclk_during_mhz": clk}
+           "per_launch_bytes": per_launch,
+           "sclk_during_mhz": (round(sum(samples) / len(samples)) if samples else None),
+           "sclk_samples": len(samples), "sclk_min_mhz": min(samples) if samples else None}
     del inp, out, ws_buf
     torch.cuda.empty_cache()
     return res
 
 
-def rooflines(name, launch_ms, per_launch):
+def rooflines(name, launch_ms, per_launch, sclk_mhz=None):
     """HBM roofline of the dominant kernel (algorithmic bytes over the
     event-timed launch, PMC traffic from profiles/pmc_<config>.json) and the
     VALU issue figures that bind these kernels."""
@@ -405,6 +431,9 @@ def rooflines(name, launch_ms, per_launch):
                 "mean_cycles_per_valu_instr": m,
                 "floor_ms": round(floor_ms, 4),
                 "frac": round(floor_ms / launch_ms, 4),
+                **({"floor_ms_at_timed_sclk": round(floor_ms * 2400.0 / sclk_mhz, 4),
+                    "frac_at_timed_sclk": round(floor_ms * 2400.0 / sclk_mhz / launch_ms, 4),
+                    "timed_sclk_mhz": sclk_mhz} if sclk_mhz else {}),
                 "source": "profiles/isa_mix.json (mixed-stream model) x profiles/round1/valu_bank_seq_probe.json (cost)"}
     return roof, valu
 
@@ -475,7 +504,8 @@ def main():
     r = time_device_config(name, dev, args.steps, args.warmup, args.prewarm_ms,
                            ws, rank, args.dist_backend, args.unbinned, probe)
     value = r["n"] * ws / (r["ms_per_step"] / 1e3)
-    roof, valu = rooflines(name, r["launch_ms"], r["per_launch_bytes"])
+    roof, valu = rooflines(name, r["launch_ms"], r["per_launch_bytes"],
+                           r["sclk_during_mhz"])
     alg = cfg["alg"]
     line = {
         "metric": metric_of(name),
@@ -524,7 +554,8 @@ def extra_configs(args, dev, probe, ws=1, rank=0):
     for name in ("c3", "c4"):
         r = time_device_config(name, dev, args.steps, min(args.warmup, 10),
                                200.0, clock_probe=probe)
-        roof, valu = rooflines(name, r["launch_ms"], r["per_launch_bytes"])
+        roof, valu = rooflines(name, r["launch_ms"], r["per_launch_bytes"],
+                           r["sclk_during_mhz"])
         out[name] = {"metric": metric_of(name), "value": round(r["n"] / (r["ms_per_step"] / 1e3), 1),
                      "unit": unit_of(name), "steps": args.steps,
                      "ms_per_step": round(r["ms_per_step"], 4),

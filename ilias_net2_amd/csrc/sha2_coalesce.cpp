@@ -459,9 +459,13 @@ int Coalescer::launch_and_wait(Slot &s, int ordinal, int *hip_err)
 	uint32_t *d_done;
 
 	CO_TRY(hipSetDevice(ordinal));
-	if (s.stream == nullptr) {
+	/* each resource is created once and kept; a failed creation leaves its
+	 * field null, so the next batch retries just that one */
+	if (s.stream == nullptr)
 		CO_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+	if (s.ev == nullptr)
 		CO_TRY(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+	if (s.h_done == nullptr) {
 		CO_TRY(hipHostMalloc((void **)&s.h_done, 64,
 		    hipHostMallocMapped | hipHostMallocCoherent));
 		*s.h_done = 0;

@@ -48,6 +48,8 @@ def lib() -> ctypes.CDLL:
                                         ctypes.c_uint64, ctypes.c_uint32, sz,
                                         vp, ctypes.c_int]
         L.oracle_sha2_batch.restype = ctypes.c_int
+        L.oracle_sha2_batch_ex.argtypes = L.oracle_sha2_batch.argtypes + [ctypes.c_int]
+        L.oracle_sha2_batch_ex.restype = ctypes.c_int
         L.oracle_ph_to_iv.argtypes = [ctypes.c_uint32, ctypes.c_uint32, sz, vp]
         L.oracle_ph_to_iv.restype = ctypes.c_int
         for pfx in ("sha256", "sha384", "sha512"):
@@ -84,16 +86,18 @@ def _ptr(a):
 
 
 def batch(alg: int, data: np.ndarray, offsets=None, lens=None, stride=0,
-          length=0, n=None, nthreads=1) -> np.ndarray:
-    """CPU digests of a packet batch, same layouts as net2_sha2_batch."""
+          length=0, n=None, nthreads=1, unrolled=False) -> np.ndarray:
+    """CPU digests of a packet batch, same layouts as net2_sha2_batch;
+    unrolled=True runs the SHA2_UNROLL_TRANSFORM form of the transforms."""
     data = np.ascontiguousarray(data, dtype=np.uint8)
     if offsets is not None:
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         lens = np.ascontiguousarray(lens, dtype=np.uint32)
         n = len(offsets)
     out = np.empty((n, DIGEST_LEN[alg]), dtype=np.uint8)
-    rc = lib().oracle_sha2_batch(alg, _ptr(data), _ptr(offsets), _ptr(lens),
-                                 stride, length, n, _ptr(out), nthreads)
+    rc = lib().oracle_sha2_batch_ex(alg, _ptr(data), _ptr(offsets), _ptr(lens),
+                                    stride, length, n, _ptr(out), nthreads,
+                                    int(unrolled))
     if rc != 0:
         raise ValueError(f"bad alg {alg}")
     return out

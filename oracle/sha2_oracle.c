@@ -185,6 +185,70 @@ void oracle_sha512_transform(uint64_t st[8], const uint8_t blk[128])
 	st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
+/*
+ * The unrolled variants (src/sha2.c:316-370 / :605-659, built there under
+ * SHA2_UNROLL_TRANSFORM): eight rounds per loop trip, the working variables
+ * renamed per round instead of shifted, so each round only writes d and h.
+ * Same digests as the rolled forms above (tests/test_oracle.py); the CPU
+ * baseline times both.
+ */
+#define UROUND(T, S1, S0, a, b, c, d, e, f, g, h, kt, x) do {		\
+	T t1_ = (h) + S1(e) + (((e) & (f)) ^ (~(e) & (g))) + (kt) + (x);	\
+	(d) += t1_;							\
+	(h) = t1_ + S0(a) + (((a) & (b)) ^ ((a) & (c)) ^ ((b) & (c)));	\
+} while (0)
+
+#define UROUNDS8(T, S1, S0, K, X)  do {					\
+	UROUND(T, S1, S0, a, b, c, d, e, f, g, h, K[t + 0], X(t + 0));	\
+	UROUND(T, S1, S0, h, a, b, c, d, e, f, g, K[t + 1], X(t + 1));	\
+	UROUND(T, S1, S0, g, h, a, b, c, d, e, f, K[t + 2], X(t + 2));	\
+	UROUND(T, S1, S0, f, g, h, a, b, c, d, e, K[t + 3], X(t + 3));	\
+	UROUND(T, S1, S0, e, f, g, h, a, b, c, d, K[t + 4], X(t + 4));	\
+	UROUND(T, S1, S0, d, e, f, g, h, a, b, c, K[t + 5], X(t + 5));	\
+	UROUND(T, S1, S0, c, d, e, f, g, h, a, b, K[t + 6], X(t + 6));	\
+	UROUND(T, S1, S0, b, c, d, e, f, g, h, a, K[t + 7], X(t + 7));	\
+} while (0)
+
+void oracle_sha256_transform_unrolled(uint32_t st[8], const uint8_t blk[64])
+{
+	uint32_t w[16];
+	uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+	uint32_t e = st[4], f = st[5], g = st[6], h = st[7];
+	int t;
+
+#define LOAD256(i) (w[i] = load_be32(blk + 4 * (i)))
+#define NEXT256(i) (w[(i) & 15] += SML0_256(w[((i) + 1) & 15]) +		\
+	w[((i) + 9) & 15] + SML1_256(w[((i) + 14) & 15]))
+	for (t = 0; t < 16; t += 8)
+		UROUNDS8(uint32_t, BIG1_256, BIG0_256, k32, LOAD256);
+	for (; t < 64; t += 8)
+		UROUNDS8(uint32_t, BIG1_256, BIG0_256, k32, NEXT256);
+#undef LOAD256
+#undef NEXT256
+	st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+	st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+void oracle_sha512_transform_unrolled(uint64_t st[8], const uint8_t blk[128])
+{
+	uint64_t w[16];
+	uint64_t a = st[0], b = st[1], c = st[2], d = st[3];
+	uint64_t e = st[4], f = st[5], g = st[6], h = st[7];
+	int t;
+
+#define LOAD512(i) (w[i] = load_be64(blk + 8 * (i)))
+#define NEXT512(i) (w[(i) & 15] += SML0_512(w[((i) + 1) & 15]) +		\
+	w[((i) + 9) & 15] + SML1_512(w[((i) + 14) & 15]))
+	for (t = 0; t < 16; t += 8)
+		UROUNDS8(uint64_t, BIG1_512, BIG0_512, k64, LOAD512);
+	for (; t < 80; t += 8)
+		UROUNDS8(uint64_t, BIG1_512, BIG0_512, k64, NEXT512);
+#undef LOAD512
+#undef NEXT512
+	st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+	st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
 /* ---- SHA-256 streaming API ---------------------------------------------- */
 
 void oracle_sha256_init(oracle_sha2_ctx *c)
@@ -373,8 +437,47 @@ int oracle_sha2_digest(int alg, const uint8_t *msg, size_t len, uint8_t *out)
 	}
 }
 
+/*
+ * One-shot digest of a contiguous message through the unrolled transforms:
+ * what Init / one Update / Final compute, with the whole blocks taken in
+ * place (src/sha2.c:479-485) and the tail padded in a local block.
+ */
+static void digest_unrolled(int alg, const uint8_t *m, size_t len, uint8_t *out)
+{
+	uint8_t tail[256];
+	const size_t bs = alg == 1 ? 64 : 128, lb = alg == 1 ? 8 : 16;
+	const size_t whole = len / bs * bs, rest = len - whole;
+	const size_t tlen = rest + 1 + lb <= bs ? bs : 2 * bs;
+	const uint64_t bits = (uint64_t)len << 3;
+
+	memcpy(tail, m + whole, rest);
+	tail[rest] = 0x80;
+	memset(tail + rest + 1, 0, tlen - rest - 1);
+	for (int i = 0; i < 8; i++)
+		tail[tlen - 1 - i] = (uint8_t)(bits >> (8 * i));
+	if (alg == 1) {
+		uint32_t st[8];
+		memcpy(st, iv256, sizeof(st));
+		for (size_t o = 0; o < whole; o += bs)
+			oracle_sha256_transform_unrolled(st, m + o);
+		for (size_t o = 0; o < tlen; o += bs)
+			oracle_sha256_transform_unrolled(st, tail + o);
+		for (int i = 0; i < 8; i++)
+			store_be32(out + 4 * i, st[i]);
+		return;
+	}
+	uint64_t st[8];
+	memcpy(st, alg == 2 ? iv384 : iv512, sizeof(st));
+	for (size_t o = 0; o < whole; o += bs)
+		oracle_sha512_transform_unrolled(st, m + o);
+	for (size_t o = 0; o < tlen; o += bs)
+		oracle_sha512_transform_unrolled(st, tail + o);
+	for (int i = 0; i < (alg == 2 ? 6 : 8); i++)
+		store_be64(out + 8 * i, st[i]);
+}
+
 struct batch_slice {
-	int alg, dlen;
+	int alg, dlen, unrolled;
 	const uint8_t *base;
 	const uint64_t *offsets;
 	const uint32_t *lens;
@@ -399,7 +502,10 @@ static void *batch_worker(void *arg)
 			m = s->base + (uint64_t)i * s->stride;
 			len = s->fixed_len;
 		}
-		oracle_sha2_digest(s->alg, m, len, s->out + i * s->dlen);
+		if (s->unrolled)
+			digest_unrolled(s->alg, m, len, s->out + i * s->dlen);
+		else
+			oracle_sha2_digest(s->alg, m, len, s->out + i * s->dlen);
 	}
 	return NULL;
 }
@@ -407,6 +513,14 @@ static void *batch_worker(void *arg)
 int oracle_sha2_batch(int alg, const uint8_t *base, const uint64_t *offsets,
     const uint32_t *lens, uint64_t stride, uint32_t fixed_len, size_t n,
     uint8_t *out, int nthreads)
+{
+	return oracle_sha2_batch_ex(alg, base, offsets, lens, stride, fixed_len,
+	    n, out, nthreads, 0);
+}
+
+int oracle_sha2_batch_ex(int alg, const uint8_t *base, const uint64_t *offsets,
+    const uint32_t *lens, uint64_t stride, uint32_t fixed_len, size_t n,
+    uint8_t *out, int nthreads, int unrolled)
 {
 	static const int dlen_of[4] = { 0, 32, 48, 64 };
 	struct batch_slice sl[256];
@@ -422,7 +536,8 @@ int oracle_sha2_batch(int alg, const uint8_t *base, const uint64_t *offsets,
 	if ((size_t)nthreads > n)
 		nthreads = n > 0 ? (int)n : 1;
 	for (t = 0; t < nthreads; t++) {
-		sl[t] = (struct batch_slice){ alg, dlen_of[alg], base, offsets,
+		sl[t] = (struct batch_slice){ alg, dlen_of[alg], unrolled != 0,
+		    base, offsets,
 		    lens, stride, fixed_len, n * t / nthreads,
 		    n * (t + 1) / nthreads, out };
 	}

@@ -49,12 +49,16 @@ void oracle_sha256_update(oracle_sha2_ctx *, const uint8_t *, size_t);
 void oracle_sha256_pad(oracle_sha2_ctx *);
 void oracle_sha256_final(uint8_t *digest, oracle_sha2_ctx *);
 void oracle_sha256_transform(uint32_t st[8], const uint8_t blk[64]);
+/* the SHA2_UNROLL_TRANSFORM form (src/sha2.c:316-370); same result */
+void oracle_sha256_transform_unrolled(uint32_t st[8], const uint8_t blk[64]);
 
 void oracle_sha512_init(oracle_sha2_ctx *);
 void oracle_sha512_update(oracle_sha2_ctx *, const uint8_t *, size_t);
 void oracle_sha512_pad(oracle_sha2_ctx *);
 void oracle_sha512_final(uint8_t *digest, oracle_sha2_ctx *);
 void oracle_sha512_transform(uint64_t st[8], const uint8_t blk[128]);
+/* the SHA2_UNROLL_TRANSFORM form (src/sha2.c:605-659); same result */
+void oracle_sha512_transform_unrolled(uint64_t st[8], const uint8_t blk[128]);
 
 void oracle_sha384_init(oracle_sha2_ctx *);
 void oracle_sha384_update(oracle_sha2_ctx *, const uint8_t *, size_t);
@@ -79,6 +83,11 @@ int oracle_sha2_digest(int alg, const uint8_t *msg, size_t len, uint8_t *out);
 int oracle_sha2_batch(int alg, const uint8_t *base, const uint64_t *offsets,
     const uint32_t *lens, uint64_t stride, uint32_t fixed_len, size_t n,
     uint8_t *out, int nthreads);
+/* Same, with unrolled != 0 running the unrolled transforms (the reference's
+ * SHA2_UNROLL_TRANSFORM build) -- the second CPU baseline of SURVEY.md 8(d). */
+int oracle_sha2_batch_ex(int alg, const uint8_t *base, const uint64_t *offsets,
+    const uint32_t *lens, uint64_t stride, uint32_t fixed_len, size_t n,
+    uint8_t *out, int nthreads, int unrolled);
 
 /*
  * HMAC (RFC 2104) over one message, for the keyed rows (alg 4..6 =

@@ -107,6 +107,32 @@ def test_batches(oracle_mod, golden):
         assert d[-1].tobytes().hex() == b["last"]
 
 
+def test_unrolled_variant(oracle_mod, golden):
+    """The SHA2_UNROLL_TRANSFORM form (src/sha2.c:316-370, :605-659) that the
+    CPU baseline also times: same digests as the rolled form on the golden
+    batches and on every padding boundary 0..300 bytes."""
+    for b in golden["batches"]:
+        if b["kind"] == "fixed":
+            data = synth.fixed_batch(b["seed"], b["n"], b["len"], b["stride"])
+            d = oracle_mod.batch(b["alg"], data, stride=b["stride"],
+                                 length=b["len"], n=b["n"], nthreads=2,
+                                 unrolled=True)
+        else:
+            lens = synth.mixed_lengths(b["len_seed"], b["n"])
+            data, offs = synth.packed(b["seed"], lens, align=b["align"])
+            d = oracle_mod.batch(b["alg"], data, offsets=offs, lens=lens,
+                                 nthreads=2, unrolled=True)
+        assert hashlib.sha256(d.tobytes()).hexdigest() == b["digest_of_digests"]
+    lens = np.arange(301, dtype=np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    data = synth.random_bytes(9, int(lens.sum()))
+    for alg, h in ((1, hashlib.sha256), (2, hashlib.sha384), (3, hashlib.sha512)):
+        d = oracle_mod.batch(alg, data, offsets=offs, lens=lens, unrolled=True)
+        for i in range(len(lens)):
+            m = bytes(data[int(offs[i]):int(offs[i]) + int(lens[i])])
+            assert d[i].tobytes() == h(m).digest(), (alg, i)
+
+
 def _ctx_digest(L, pfx, chunks, dl):
     ctx = ctypes.create_string_buffer(208)
     getattr(L, f"oracle_{pfx}_init")(ctx)
