@@ -17,6 +17,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -57,6 +58,14 @@ CONFIGS = {
                             workload="1M x mixed {64,512,1500} B datagrams, HMAC-SHA256 verify (hash field || message), binned (8f row 1, RX)"),
     "hmac512_verify_mtu": dict(alg=6, kind="dgram_verify", n=1 << 20, length=None,
                                workload="1M x mixed {64,512,1500} B datagrams, HMAC-SHA512 verify (hash field || message), binned (8f row 1, RX, the negotiated default)"),
+    # the hash steps of net2_packet_decode / _encode for a burst under one
+    # connection's keys (HMAC-SHA512 + AES-256-CBC IVs, every datagram
+    # PH_SIGNED|PH_ENCRYPTED): wire sizes {136, 584, 1500} B = 8-byte header
+    # + 64-byte HMAC field + {64, 512, 1428} B payload (8f row 3')
+    "burst_rx": dict(alg=6, kind="burst_rx", n=1 << 20, length=None, ivlen=16,
+                     workload="1M x {136,584,1500} B wire datagrams, net2_packet_decode_burst: header, HMAC-SHA512 verify, 16-B IVs (8f row 3', RX)"),
+    "burst_tx": dict(alg=6, kind="burst_tx", n=1 << 20, length=None, ivlen=16,
+                     workload="1M x {136,584,1500} B wire datagrams, net2_packet_encode_burst: header + HMAC-SHA512 field (8f row 3', TX)"),
     "ph_iv": dict(alg=1, kind="ph_iv", n=1 << 20, length=16,
                   workload="1M packet headers -> 16-byte IVs, net2_ph_to_iv_dev (8f row 3)"),
 }
@@ -87,15 +96,23 @@ def make_inputs(cfg, dev, seed):
         flags = torch.randint(0, 1 << 30, (n,), dtype=torch.int32, device=dev,
                               generator=g)
         return dict(seq=seq, flags=flags, n=n, payload=8 * n)
-    choice = torch.tensor([64, 512, 1500], dtype=torch.int64, device=dev)
+    burst = cfg["kind"].startswith("burst")
+    choice = torch.tensor([136, 584, 1500] if burst else [64, 512, 1500],
+                          dtype=torch.int64, device=dev)
     lens = choice[torch.randint(0, 3, (n,), device=dev, generator=g)]
     offs = torch.zeros(n, dtype=torch.int64, device=dev)
     offs[1:] = torch.cumsum(lens, 0)[:-1]
     total = int(lens.sum().item())
     data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev,
                          generator=g)
-    return dict(data=data, n=n, offs=offs, lens=lens.to(torch.int32),
-                payload=total)
+    r = dict(data=data, n=n, offs=offs, lens=lens.to(torch.int32), payload=total)
+    if burst:
+        r["seq"] = torch.arange(n, dtype=torch.int32, device=dev)
+        r["flags"] = torch.full((n,), 3, dtype=torch.int32, device=dev)  # SIGNED|ENCRYPTED
+        r["iv"] = torch.empty((n, cfg["ivlen"]), dtype=torch.uint8, device=dev)
+        r["oseq"] = torch.empty(n, dtype=torch.int32, device=dev)
+        r["oflags"] = torch.empty(n, dtype=torch.int32, device=dev)
+    return r
 
 
 def _cpu_model():
@@ -284,6 +301,17 @@ def device_step(name, inp, out, ws_buf, stream, unbinned=False):
     L = _lib.lib()
     n, alg = inp["n"], cfg["alg"]
     kbuf = HMAC_KEY[:DLEN[alg]] if alg >= 4 else b""
+    if cfg["kind"] == "burst_rx":
+        return lambda: _lib.check(L.net2_packet_decode_burst(
+            alg, kbuf, len(kbuf), 1, cfg["ivlen"], inp["data"].data_ptr(),
+            inp["offs"].data_ptr(), inp["lens"].data_ptr(), n, out.data_ptr(),
+            inp["iv"].data_ptr(), inp["oseq"].data_ptr(), inp["oflags"].data_ptr(),
+            ws_buf.data_ptr(), ws_buf.numel(), stream.cuda_stream))
+    if cfg["kind"] == "burst_tx":
+        return lambda: _lib.check(L.net2_packet_encode_burst(
+            alg, kbuf, len(kbuf), 1, inp["seq"].data_ptr(), inp["flags"].data_ptr(),
+            inp["data"].data_ptr(), inp["offs"].data_ptr(), inp["lens"].data_ptr(),
+            n, out.data_ptr(), ws_buf.data_ptr(), ws_buf.numel(), stream.cuda_stream))
     if cfg["kind"] == "dgram_verify":
         return lambda: _lib.check(L.net2_hmac_verify_dev(
             alg, kbuf, len(kbuf), inp["data"].data_ptr(),
@@ -319,15 +347,24 @@ def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
     on the launch stream.  Returns the measurements (max over ranks)."""
     import torch
     import torch.distributed as dist
-    from ilias_net2_amd import batch
+    from ilias_net2_amd import batch, _lib
     cfg = CONFIGS[name]
     inp = make_inputs(cfg, dev, seed=2 + rank)
     n, alg = inp["n"], cfg["alg"]
+    burst = cfg["kind"].startswith("burst")
     dlen = cfg["length"] if cfg["kind"] == "ph_iv" else \
-        1 if cfg["kind"] == "dgram_verify" else DLEN[alg]
+        1 if cfg["kind"] == "dgram_verify" or burst else DLEN[alg]
     out = torch.empty((n, dlen), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     ws_buf = batch.var_workspace(n, dev) if cfg["kind"] in ("mixed", "dgram_verify") else None
+    if burst:
+        ws_buf = torch.empty(_lib.lib().net2_packet_burst_workspace(n),
+                             dtype=torch.uint8, device=dev)
+    if cfg["kind"] == "burst_rx":
+        # encode once (untimed), so every datagram verifies and gets its IV
+        device_step("burst_tx", inp, out, ws_buf, stream)()
+        torch.cuda.synchronize(dev)
+        assert int((out != 0).sum()) == 0, "burst encode failed"
     if cfg["kind"] == "dgram_verify":
         # sign once (untimed) so every datagram verifies
         batch.hmac_sign_dev(alg, HMAC_KEY[:DLEN[alg]], inp["data"], inp["offs"],
@@ -354,21 +391,31 @@ def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
         a.record(stream)
         step()
         b.record(stream)
-    # shader clock while the queued steps run: sampled every ~2 ms until the
-    # last step's event completes (host-side reads, off the GPU's path)
-    samples = []
-    while clock_probe is not None:
-        c = clock_probe()
-        if c:
+    # shader clock while the queued steps run, sampled every ~2 ms by a
+    # helper thread (a sysfs read can take a millisecond: kept off the
+    # thread whose synchronize ends the timed region)
+    samples, stop = [], threading.Event()
+
+    def sample():
+        while not stop.is_set():
+            c = clock_probe()
+            if not c:
+                return
             samples.append(c)
-        if ev[-1][1].query() or not c:
-            break
-        time.sleep(0.002)
+            stop.wait(0.002)
+    sampler = threading.Thread(target=sample, daemon=True) if clock_probe else None
+    if sampler:
+        sampler.start()
     torch.cuda.synchronize(dev)
     if ws > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if sampler:
+        stop.set()
+        sampler.join()
     launch_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    if burst:   # every datagram of the synthetic burst is well-formed
+        assert int((out != 0).sum()) == 0, f"{name}: datagrams not OK"
 
     if ws > 1:
         t = torch.tensor([elapsed, launch_ms], dtype=torch.float64,
@@ -378,7 +425,11 @@ def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
     # algorithmic bytes: payload read + digests written (+ 12 B/packet of
     # offsets and lengths for the variable layout), per launch
     per_launch = inp["payload"] + n * dlen + \
-        (12 * n if cfg["kind"] in ("mixed", "dgram_verify") else 0)
+        (12 * n if cfg["kind"] in ("mixed", "dgram_verify") or burst else 0)
+    if cfg["kind"] == "burst_rx":     # + decoded header and IV out
+        per_launch += n * (8 + cfg["ivlen"])
+    elif cfg["kind"] == "burst_tx":   # + header in; header + field written
+        per_launch += n * (8 + 8 + DLEN[alg])
     res = {"n": n, "dlen": dlen, "payload": inp["payload"], "elapsed": elapsed,
            "ms_per_step": elapsed * 1e3 / steps, "launch_ms": launch_ms,
            "per_launch_bytes": per_launch,
@@ -445,12 +496,14 @@ def metric_of(name):
         return METRIC
     return (("SHA-256 IVs/s, " if cfg["kind"] == "ph_iv" else
              f"{ALG_NAMES[alg]} datagrams verified/s, " if cfg["kind"] == "dgram_verify" else
+             "datagrams decoded/s, " if cfg["kind"] == "burst_rx" else
+             "datagrams encoded/s, " if cfg["kind"] == "burst_tx" else
              f"{ALG_NAMES[alg]} digests/s, ") + cfg["workload"])
 
 
 def unit_of(name):
     kind = CONFIGS[name]["kind"]
-    return "datagrams/s" if kind == "dgram_verify" else "IVs/s" if kind == "ph_iv" else "digests/s"
+    return "datagrams/s" if kind in ("dgram_verify", "burst_rx", "burst_tx") else "IVs/s" if kind == "ph_iv" else "digests/s"
 
 
 def main():

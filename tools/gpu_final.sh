@@ -5,7 +5,7 @@ set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 ROUND=${ROUND:-round2}
-PC="${PCFGS:-c2 c4 c3 c3_512 hmac hmac_mtu hmac512 hmac512_mtu hmac_verify_mtu hmac512_verify_mtu}"
+PC="${PCFGS:-c2 c4 c3 c3_512 hmac hmac_mtu hmac512 hmac512_mtu hmac_verify_mtu hmac512_verify_mtu burst_rx burst_tx}"
 CFGS="$PC" bash tools/gpu_profile.sh
 rc=$?; echo "profile rc=$rc"; [ $rc -ne 0 ] && exit $rc
 mkdir -p gpurun_out/profiles_$ROUND

@@ -56,6 +56,8 @@ KERNELS = {
     "c3_512": "_ZN4net23dev10var_kernelINS0_6Sha512E",
     "hmac_verify_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha256TILb1ELb1ELb0EEELb0ELi2E",
     "hmac512_verify_mtu": "_ZN4net23dev11hmac_kernelINS0_6Sha512ELb0ELi2E",
+    "burst_rx": "_ZN4net23dev11hmac_kernelINS0_6Sha512ELb0ELi2E",
+    "burst_tx": "_ZN4net23dev11hmac_kernelINS0_6Sha512ELb0ELi1E",
 }
 
 # probe row name -> (mnemonic, operand form); form "v" = VGPR/inline-constant

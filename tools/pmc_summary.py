@@ -33,7 +33,8 @@ KERNEL = {"c2": "fixed_kernel<net2::dev::Sha256", "c4": "fixed_kernel<net2::dev:
           "hmac_mtu": "hmac_kernel<net2::dev::Sha256", "ph_iv": "ph_iv_kernel",
           "hmac512": "hmac_kernel<net2::dev::Sha512", "hmac512_mtu": "hmac_kernel<net2::dev::Sha512",
           "hmac_verify_mtu": "hmac_kernel<net2::dev::Sha256",
-          "hmac512_verify_mtu": "hmac_kernel<net2::dev::Sha512"}
+          "hmac512_verify_mtu": "hmac_kernel<net2::dev::Sha512",
+          "burst_rx": "hmac_kernel<net2::dev::Sha512", "burst_tx": "hmac_kernel<net2::dev::Sha512"}
 
 
 def per_dispatch(path, pattern):

@@ -16,7 +16,9 @@ import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = {"c2": "fixed_kernel<net2::dev::Sha256", "c4": "fixed_kernel<net2::dev::Sha512",
-          "c3": "var_kernel<net2::dev::Sha256", "c3_512": "var_kernel<net2::dev::Sha512"}
+          "c3": "var_kernel<net2::dev::Sha256", "c3_512": "var_kernel<net2::dev::Sha512",
+          "hmac512_verify_mtu": "hmac_kernel<net2::dev::Sha512",
+          "burst_rx": "hmac_kernel<net2::dev::Sha512", "burst_tx": "hmac_kernel<net2::dev::Sha512"}
 ALGO = {"c2": 1 << 30, "c4": 1 << 30, "c3": None}
 
 
