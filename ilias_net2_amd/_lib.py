@@ -61,6 +61,9 @@ SIGNATURES = {
         ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
         ctypes.POINTER(IOVec), ctypes.c_size_t, ctypes.c_void_p,
         ctypes.c_size_t]),
+    "net2_coalesce_stats": (ctypes.c_int, [
+        ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+        ctypes.POINTER(ctypes.c_uint64)]),
     "net2_hmac_dev": (ctypes.c_int, [
         ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,

@@ -157,6 +157,13 @@ public:
 	}
 
 	int submit(int ordinal, const Request &r, int *hip_err);
+	void stats(uint64_t *calls, uint64_t *launches) const
+	{
+		if (calls)
+			*calls = calls_.load(std::memory_order_relaxed);
+		if (launches)
+			*launches = launches_.load(std::memory_order_relaxed);
+	}
 
 private:
 	int grow_stage(Slot &s, size_t need, int ordinal);
@@ -173,6 +180,7 @@ private:
 	int open_ = -1;
 	std::vector<int> free_;
 	int inflight_ = 0;
+	std::atomic<uint64_t> calls_{0}, launches_{0};
 };
 
 int Coalescer::grow_stage(Slot &s, size_t need, int ordinal)
@@ -382,6 +390,8 @@ int Coalescer::submit(int ordinal, const Request &r, int *hip_err)
 
 	int herr = 0;
 	const int rc = launch_and_wait(s, ordinal, &herr);
+	launches_.fetch_add(1, std::memory_order_relaxed);
+	calls_.fetch_add(s.jobs.size(), std::memory_order_relaxed);
 	if (rc == EIO && hip_err != nullptr)
 		*hip_err = herr;
 	for (Job *jp : s.jobs) {
@@ -571,6 +581,24 @@ Coalescer *coalescer(size_t idx)
 }
 
 }	/* namespace */
+
+void stats(size_t idx, uint64_t *calls, uint64_t *launches)
+{
+	Coalescer *c = nullptr;
+	{
+		std::lock_guard<std::mutex> g(g_mu);
+		if (idx < g_co.size())
+			c = g_co[idx].get();
+	}
+	if (c != nullptr) {
+		c->stats(calls, launches);
+		return;
+	}
+	if (calls)
+		*calls = 0;
+	if (launches)
+		*launches = 0;
+}
 
 int submit(size_t idx, int ordinal, const Request &r, int *hip_err)
 {

@@ -46,6 +46,10 @@ struct Request {
  */
 int submit(size_t idx, int ordinal, const Request &r, int *hip_err);
 
+/* Requests served and launches made by coalescer idx (0, 0 before its
+ * first request). */
+void stats(size_t idx, uint64_t *calls, uint64_t *launches);
+
 }	/* namespace net2co */
 
 /*

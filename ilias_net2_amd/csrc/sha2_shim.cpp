@@ -618,6 +618,19 @@ int net2_co_run(const net2co::Request &r)
 
 /* ---- exported C ABI ---------------------------------------------------- */
 
+NET2_EXPORT int net2_coalesce_stats(int device, uint64_t *calls,
+    uint64_t *launches)
+{
+	const std::vector<int> &dv = devices();
+	if (dv.empty())
+		return ENODEV;
+	if (device < -1 || device >= (int)dv.size())
+		return EINVAL;
+	net2co::stats(device < 0 ? small_device(dv) : (size_t)device, calls,
+	    launches);
+	return 0;
+}
+
 NET2_EXPORT const int net2_hashmax = kNumRows;
 
 NET2_EXPORT int net2_sha2_abi_version(void)

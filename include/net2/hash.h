@@ -66,6 +66,17 @@ int net2_hashctx_hashiov(int alg, const void *key, size_t keylen,
     const struct iovec *iov, size_t iovcnt, void *out, size_t outlen);
 
 /*
+ * Counters of the request coalescer behind the single-message calls
+ * (net2_hashctx_hashiov, the SHA2_CTX calls of net2/sha2.h, net2_ph_to_iv)
+ * on gfx950 device `device` (an index into the devices these calls use; -1
+ * = the one the calling thread's calls go to): requests served and kernel
+ * launches they took since the process started.  calls / launches is the
+ * mean batch size.  Either pointer may be NULL.  0, EINVAL (no such
+ * device) or ENODEV.
+ */
+int net2_coalesce_stats(int device, uint64_t *calls, uint64_t *launches);
+
+/*
  * Batched keyed hash (HMAC, RFC 2104) of many packets under one key -- the
  * per-datagram authenticator of net2_packet_encode/decode
  * (types/packet.n2t:246,417) for a whole receive or transmit batch.

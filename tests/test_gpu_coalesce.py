@@ -9,6 +9,7 @@ state, bit count and the buffer as src/sha2.c leaves it
 (src/sha2.c:449-563, :738-919).
 """
 import ctypes
+import errno
 import threading
 
 import numpy as np
@@ -203,37 +204,54 @@ def test_many_threads_mixed(L, oracle_mod):
     assert not errors, errors[:5]
 
 
+def _stats(L):
+    c, n = ctypes.c_uint64(), ctypes.c_uint64()
+    assert L.net2_coalesce_stats(-1, ctypes.byref(c), ctypes.byref(n)) == 0
+    return c.value, n.value
+
+
 def test_coalesced_batches_form(L, oracle_mod):
     """Under concurrency the calls really share launches: 32 threads x 50
-    calls of a 1 KiB SHA-512 finish well within the time the calls would
-    take one after another.  (Python's per-call overhead, under the GIL,
-    caps the speed-up here at ~3x; tools/coalesce_bench.c measures the
-    library itself: ~30x at 64 threads, DESIGN.md.)"""
-    import time
-    from ilias_net2_amd import hash as h
+    calls of a 1 KiB SHA-512 straight through net2_hashctx_hashiov (ctypes
+    drops the GIL for the call, so the calls overlap in the library) take
+    far fewer launches than calls (net2_coalesce_stats), and every digest is
+    right.  tools/coalesce_bench.c measures the rates."""
+    from ilias_net2_amd import _lib
     m = bytes(range(256)) * 4
     want = oracle_mod.digest(3, m)
-    h.hashbuf(3, b"", m)
-    t0 = time.perf_counter()
-    for _ in range(50):
-        assert h.hashbuf(3, b"", m) == want
-    single = (time.perf_counter() - t0) / 50
+    buf = ctypes.create_string_buffer(m, len(m))
+    iov = (_lib.IOVec * 1)()
+    iov[0].iov_base = ctypes.cast(buf, ctypes.c_void_p)
+    iov[0].iov_len = len(m)
+
+    def one():
+        out = ctypes.create_string_buffer(64)
+        assert L.net2_hashctx_hashiov(3, None, 0, iov, 1, out, 64) == 0
+        return out.raw
+    assert one() == want
+    c0, n0 = _stats(L)
+    for _ in range(20):              # one at a time: a launch per call
+        one()
+    c1, n1 = _stats(L)
+    assert (c1 - c0, n1 - n0) == (20, 20)
     bad = []
 
     def worker():
         for _ in range(50):
-            if h.hashbuf(3, b"", m) != want:
+            if one() != want:
                 bad.append(1)
     ths = [threading.Thread(target=worker) for _ in range(32)]
-    t0 = time.perf_counter()
     for t in ths:
         t.start()
     for t in ths:
         t.join()
-    el = time.perf_counter() - t0
+    c2, n2 = _stats(L)
     assert not bad
-    # 1,600 calls; serialised they would take 1600 * single
-    assert el < 1600 * single / 2, (el, single)
+    assert c2 - c1 == 1600
+    # 1,600 calls from 32 threads: batches of several calls each
+    assert n2 - n1 < 1600 / 2, (c2 - c1, n2 - n1)
+    # the stats of a device index out of range
+    assert L.net2_coalesce_stats(99, None, None) == errno.EINVAL
 
 
 _FORM_CHECK = r'''
