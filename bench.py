@@ -36,6 +36,10 @@ CONFIGS = {
                workload="1M x mixed {64,512,1500} B packets, SHA-256, length-binned (configs[2])"),
     "c4": dict(alg=3, kind="fixed", n=1 << 20, length=1024,
                workload="1M x 1 KiB packets, SHA-512, device-resident (configs[3])"),
+    # byte-aligned packet starts (lengths not multiples of 4): the A1 load
+    # path of the variable-length kernel (not a BASELINE config)
+    "c3_a1": dict(alg=1, kind="mixed", n=1 << 20, length=None, choice=[63, 511, 1499],
+                  workload="1M x mixed {63,511,1499} B packets (byte-aligned starts), SHA-256, length-binned"),
     # the negotiated sighash (SHA-512) over variable-length payloads: the
     # signed-carver flow's shape (not a BASELINE config)
     "c3_512": dict(alg=3, kind="mixed", n=1 << 20, length=None,
@@ -97,7 +101,7 @@ def make_inputs(cfg, dev, seed):
                               generator=g)
         return dict(seq=seq, flags=flags, n=n, payload=8 * n)
     burst = cfg["kind"].startswith("burst")
-    choice = torch.tensor([136, 584, 1500] if burst else [64, 512, 1500],
+    choice = torch.tensor([136, 584, 1500] if burst else cfg.get("choice", [64, 512, 1500]),
                           dtype=torch.int64, device=dev)
     lens = choice[torch.randint(0, 3, (n,), device=dev, generator=g)]
     offs = torch.zeros(n, dtype=torch.int64, device=dev)

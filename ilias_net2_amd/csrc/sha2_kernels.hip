@@ -662,8 +662,16 @@ __device__ __forceinline__ void var_digest(const uint8_t *p, uint32_t len,
  * workgroup) of one whole-block length, e.g. a bin of a batch of fixed
  * sizes, takes its pad schedule from g_padtab256 (g_padtab512).
  */
+#ifndef NET2_VAR_WAVES
+#define NET2_VAR_WAVES 0
+#endif
+#if NET2_VAR_WAVES > 0
+#define NET2_VAR_ATTR __attribute__((amdgpu_waves_per_eu(NET2_VAR_WAVES)))
+#else
+#define NET2_VAR_ATTR
+#endif
 template <class H>
-__global__ __launch_bounds__(256) void var_kernel(const uint8_t *__restrict__ base,
+__global__ __launch_bounds__(256) NET2_VAR_ATTR void var_kernel(const uint8_t *__restrict__ base,
     const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
     const uint32_t *__restrict__ perm, uint64_t n, uint8_t *__restrict__ out,
     uint32_t dlen, int is384)
