@@ -436,11 +436,27 @@ void pack_fill(WorkPool &pool, const PackPlan &pl, uint8_t *dst, uint64_t *dst_o
 }
 
 /*
+ * Digests of the host path: the kernel stores them straight into pinned
+ * host memory (the caller's buffer when it is pinned, else the slot's
+ * staging) through its device mapping, so a chunk costs one H2D copy and no
+ * D2H copy.  With a D2H copy per chunk the copies of every slot shared one
+ * DMA queue in submission order: chunk k's D2H, waiting for its kernel,
+ * held chunk k+1's H2D back, and the path ran at 91 % of the link's copy
+ * rate.  NET2_SHA2_D2H_COPY=1 restores the copy (A/B).
+ */
+bool d2h_copy()
+{
+	static const bool on = getenv("NET2_SHA2_D2H_COPY") != nullptr &&
+	    atoi(getenv("NET2_SHA2_D2H_COPY")) != 0;
+	return on;
+}
+
+/*
  * One chunk [lo, hi) of the caller's packets into slot s: H2D (straight from
  * the caller's buffer when it is pinned and the layout is fixed, else
  * through the slot's pinned staging, packed with 16-byte aligned packet
- * starts), kernel, D2H of the digests (straight into the caller's buffer
- * when that is pinned).
+ * starts), kernel writing the digests to pinned host memory (the caller's
+ * buffer when that is pinned).
  */
 int enqueue_chunk(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
     const uint64_t *offsets, const uint32_t *lens, uint64_t stride,
@@ -465,13 +481,27 @@ int enqueue_chunk(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
 		return rc;
 	if (dbg_timing())
 		fprintf(stderr, "net2: reserve %.3f ms\n", dbg_now() - tr0);
+	/* where the kernel stores the digests (see d2h_copy) */
+	uint8_t *const host_dig = dst_pinned ? user_dig : s.h_dig;
+	uint8_t *kout = s.d_dig;
+	bool direct = false;
+	if (!d2h_copy()) {
+		void *dp = nullptr;
+		if (hipHostGetDevicePointer(&dp, host_dig, 0) == hipSuccess &&
+		    dp != nullptr) {
+			kout = static_cast<uint8_t *>(dp);
+			direct = true;
+		} else {
+			(void)hipGetLastError();
+		}
+	}
 
 	if (offsets == nullptr && src_pinned) {
 		if (bytes != 0)
 			HIP_TRY(hipMemcpyAsync(s.d_in, base + lo * stride,
 			    bytes, hipMemcpyHostToDevice, s.stream));
 		HIP_TRY(net2_launch_fixed(alg, s.d_in, stride, fixed_len, n,
-		    s.d_dig, s.stream));
+		    kout, s.stream));
 	} else if (offsets == nullptr) {
 		const size_t st = (fixed_len + 15) & ~15u;
 		if (st == stride) {
@@ -494,7 +524,7 @@ int enqueue_chunk(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
 			HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
 			    hipMemcpyHostToDevice, s.stream));
 		HIP_TRY(net2_launch_fixed(alg, s.d_in, st, fixed_len, n,
-		    s.d_dig, s.stream));
+		    kout, s.stream));
 	} else {
 		const double tg0 = dbg_now();
 		pack_fill(pool, plan, s.h_in, s.h_off, s.h_len, base, offsets + lo,
@@ -510,10 +540,11 @@ int enqueue_chunk(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
 		HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, n * 4,
 		    hipMemcpyHostToDevice, s.stream));
 		HIP_TRY(net2_launch_var(alg, s.d_in, s.d_off, s.d_len, n,
-		    s.d_dig, n >= 4096 ? s.d_ws : nullptr, s.stream));
+		    kout, n >= 4096 ? s.d_ws : nullptr, s.stream));
 	}
-	HIP_TRY(hipMemcpyAsync(dst_pinned ? user_dig : s.h_dig, s.d_dig,
-	    (size_t)n * dl, hipMemcpyDeviceToHost, s.stream));
+	if (!direct)
+		HIP_TRY(hipMemcpyAsync(host_dig, s.d_dig, (size_t)n * dl,
+		    hipMemcpyDeviceToHost, s.stream));
 	HIP_TRY(hipEventRecord(s.done, s.stream));
 	s.busy = true;
 	s.user_dig = dst_pinned ? nullptr : user_dig;
