@@ -153,6 +153,24 @@ struct Sha512 {
 	}
 };
 
+/* SHA-512 for the variable-length kernel; NET2_VAR512_PF=1 (A/B only)
+ * gives it the two-block ping-pong prefetch the SHA-256 kernels have. */
+#ifndef NET2_VAR512_PF
+#define NET2_VAR512_PF 0
+#endif
+struct Sha512V : Sha512 {
+	static constexpr bool U2 = NET2_VAR512_PF != 0;
+	static constexpr bool PREFETCH = NET2_VAR512_PF != 0;
+};
+/* ... and for the variable-length HMAC kernels (NET2_HMAC512_PF) */
+#ifndef NET2_HMAC512_PF
+#define NET2_HMAC512_PF 0
+#endif
+struct Sha512H : Sha512 {
+	static constexpr bool U2 = NET2_HMAC512_PF != 0;
+	static constexpr bool PREFETCH = NET2_HMAC512_PF != 0;
+};
+
 /* ---- message loading ------------------------------------------------- */
 
 /*
@@ -1807,7 +1825,7 @@ hipError_t net2_launch_var(int alg, const uint8_t *base,
 		var_kernel<Sha256V><<<grid_for(n), 256, 0, s>>>(base, offsets,
 		    lens, perm, n, out, dlen, 0);
 	else
-		var_kernel<Sha512><<<grid_for(n), 256, 0, s>>>(base, offsets,
+		var_kernel<Sha512V><<<grid_for(n), 256, 0, s>>>(base, offsets,
 		    lens, perm, n, out, dlen, is384);
 	return hipGetLastError();
 }
@@ -1894,7 +1912,7 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 			hmac_kernel<Sha512, true><<<grid, 256, 0, s>>>(base, offsets,
 			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad);
 		} else if (offsets != nullptr) {
-			launch_hmac_var_mode<Sha512>(mode, grid, s, base, offsets,
+			launch_hmac_var_mode<Sha512H>(mode, grid, s, base, offsets,
 			    lens, perm, n, out, dlen, is384, k, pad);
 		} else {
 			hmac_kernel<Sha512, false><<<grid, 256, 0, s>>>(base, offsets,

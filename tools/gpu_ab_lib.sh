@@ -3,7 +3,7 @@
 set -u
 mkdir -p gpurun_out
 : > gpurun_out/ab_lib.txt
-for r in 1 2; do
+for r in ${REPS:-1 2}; do
   for c in ${CFGS:-c2 c3 hmac hmac_mtu}; do
     for lib in default tools/ab/*.so; do
       if [ "$lib" = default ]; then unset NET2_SHA2_LIB; else export NET2_SHA2_LIB=$PWD/$lib; fi

@@ -52,12 +52,12 @@ KERNELS = {
     "hmac": "_ZN4net23dev11hmac_kernelINS0_7Sha256TILb1ELb1ELb1EEELb1E",
     "hmac_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha256TILb1ELb1ELb1EEELb0ELi0E",
     "hmac512": "_ZN4net23dev11hmac_kernelINS0_6Sha512ELb1E",
-    "hmac512_mtu": "_ZN4net23dev11hmac_kernelINS0_6Sha512ELb0ELi0E",
-    "c3_512": "_ZN4net23dev10var_kernelINS0_6Sha512E",
+    "hmac512_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha512HELb0ELi0E",
+    "c3_512": "_ZN4net23dev10var_kernelINS0_7Sha512VE",
     "hmac_verify_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha256TILb1ELb1ELb0EEELb0ELi2E",
-    "hmac512_verify_mtu": "_ZN4net23dev11hmac_kernelINS0_6Sha512ELb0ELi2E",
-    "burst_rx": "_ZN4net23dev11hmac_kernelINS0_6Sha512ELb0ELi2E",
-    "burst_tx": "_ZN4net23dev11hmac_kernelINS0_6Sha512ELb0ELi1E",
+    "hmac512_verify_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha512HELb0ELi2E",
+    "burst_rx": "_ZN4net23dev11hmac_kernelINS0_7Sha512HELb0ELi2E",
+    "burst_tx": "_ZN4net23dev11hmac_kernelINS0_7Sha512HELb0ELi1E",
 }
 
 # probe row name -> (mnemonic, operand form); form "v" = VGPR/inline-constant
