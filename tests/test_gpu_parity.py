@@ -276,6 +276,79 @@ def test_host_batch(dev, batch, oracle_mod):
     assert np.array_equal(got, want)
 
 
+def test_host_batch_digests_to_mapped_memory(dev, batch, oracle_mod):
+    """The host path stores digests straight into pinned host memory through
+    its device mapping: registered (hipHostRegister) memory at an interior,
+    odd offset; the variable layout into pinned memory; and the D2H-copy
+    fallback of the same calls in a child process (NET2_SHA2_D2H_COPY=1)."""
+    from ilias_net2_amd import _lib
+    L = _lib.lib()
+    n, length = 30000, 700
+    data = synth.random_bytes(31, n * length)
+    want = oracle_mod.batch(3, data, stride=length, length=length, n=n,
+                            nthreads=CPU_THREADS)
+    # a registered page-aligned buffer; digests written from byte 13 on
+    buf = np.zeros(n * 64 + 8192, dtype=np.uint8)
+    base = buf.ctypes.data
+    a0 = (base + 4095) & ~4095
+    span = n * 64 + 4096
+    cr = torch.cuda.cudart()
+    assert int(cr.cudaHostRegister(a0, span, 0)) == 0
+    try:
+        at = a0 + 13
+        rc = L.net2_sha2_batch(3, data.ctypes.data, None, None, length, length,
+                               n, at, 1)
+        assert rc == 0
+        got = buf[at - base: at - base + n * 64].reshape(n, 64)
+        assert np.array_equal(got, want)
+        assert not buf[:at - base].any()          # nothing outside the range
+        assert not buf[at - base + n * 64:].any()
+    finally:
+        assert int(cr.cudaHostUnregister(a0)) == 0
+    # variable layout (binned, scattered digest stores) into pinned memory
+    lens = synth.mixed_lengths(32, 40000)
+    data, offs = synth.packed(33, lens)
+    out = torch.zeros((len(lens), 32), dtype=torch.uint8).pin_memory()
+    o64 = np.ascontiguousarray(offs, dtype=np.uint64)   # kept alive for the call
+    l32 = np.ascontiguousarray(lens, dtype=np.uint32)
+    rc = L.net2_sha2_batch(1, data.ctypes.data, o64.ctypes.data, l32.ctypes.data,
+                           0, 0, len(lens), out.data_ptr(), 1)
+    assert rc == 0
+    assert np.array_equal(out.numpy(), oracle_mod.batch(1, data, offsets=offs, lens=lens,
+                                                        nthreads=CPU_THREADS))
+
+
+def test_host_batch_d2h_copy_fallback(dev):
+    """NET2_SHA2_D2H_COPY=1 (the D2H-copy form, kept for A/B) gives the same
+    digests as the default form, pinned and pageable outputs alike."""
+    import subprocess
+    import sys
+    code = r'''
+import sys
+sys.path.insert(0, ".")
+sys.path.insert(0, "tests")
+import numpy as np
+import torch
+import synth
+from oracle import oracle
+from ilias_net2_amd import batch, _lib
+data = synth.fixed_batch(34, 20000, 1024)
+want = oracle.batch(1, data, stride=1024, length=1024, n=20000, nthreads=4)
+assert np.array_equal(batch.digest_host(1, data, stride=1024, length=1024, n=20000), want)
+out = torch.empty((20000, 32), dtype=torch.uint8).pin_memory()
+assert _lib.lib().net2_sha2_batch(1, data.ctypes.data, None, None, 1024, 1024, 20000,
+                                  out.data_ptr(), 1) == 0
+assert np.array_equal(out.numpy(), want)
+print("ok")
+'''
+    import os
+    env = dict(os.environ, NET2_SHA2_D2H_COPY="1")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
 def test_host_batch_var_multichunk(dev, batch, oracle_mod):
     """Variable layout from pageable memory over several 64 MiB chunks whose
     byte and packet counts differ (staging growth, parallel gather), twice
