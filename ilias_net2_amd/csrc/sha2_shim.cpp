@@ -128,6 +128,22 @@ std::vector<int> batch_devices()
 	return dv;
 }
 
+/*
+ * Least payload per device slice of net2_sha2_batch (NET2_SHA2_SLICE_MIN_BYTES,
+ * read per call; default 16 MiB, 0 = no limit).  A small batch's latency is
+ * one lane's serial chain of compressions, which more devices do not
+ * shorten, while each extra device costs a host thread, its own copies and
+ * a synchronisation: a 4096 x 1 KiB signing tick stays on one GPU, a 1 GiB
+ * batch spreads over eight.
+ */
+uint64_t slice_min_bytes()
+{
+	const char *v = getenv("NET2_SHA2_SLICE_MIN_BYTES");
+	if (v == nullptr || *v == '\0')
+		return 16ull << 20;
+	return strtoull(v, nullptr, 10);
+}
+
 /* Is the calling thread's current device one we built code for? */
 int check_current_device()
 {
@@ -762,6 +778,17 @@ NET2_EXPORT int net2_sha2_batch(int alg, const void *base,
 		nd = (size_t)max_devices;
 	if ((uint64_t)nd > n)
 		nd = (size_t)n;
+	uint64_t total = 0;
+	if (offsets == nullptr) {
+		total = n * (uint64_t)fixed_len;
+	} else {
+		for (uint64_t i = 0; i < n; i++)
+			total += lens[i];
+	}
+	const uint64_t min_slice = slice_min_bytes();
+	if (min_slice > 0 && nd > 1)
+		nd = (size_t)std::max<uint64_t>(1, std::min<uint64_t>(nd,
+		    total / min_slice));
 
 	/* Contiguous slices: by packet count, or by bytes for var layout. */
 	std::vector<uint64_t> cut(nd + 1, 0);
@@ -770,9 +797,7 @@ NET2_EXPORT int net2_sha2_batch(int alg, const void *base,
 		for (size_t d = 1; d < nd; d++)
 			cut[d] = n * d / nd;
 	} else {
-		uint64_t total = 0, acc = 0;
-		for (uint64_t i = 0; i < n; i++)
-			total += lens[i];
+		uint64_t acc = 0;
 		size_t d = 1;
 		for (uint64_t i = 0; i < n && d < nd; i++) {
 			acc += lens[i];

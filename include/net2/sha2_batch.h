@@ -86,16 +86,19 @@ int net2_sha2_dev_var(int alg, const void *d_base, const uint64_t *d_offsets,
 size_t net2_sha2_dev_var_workspace(uint64_t n);
 
 /*
- * Host-memory batch, end to end: packets are read from host memory,
- * staged through pinned buffers to every usable device (contiguous packet
- * slices, one host thread and stream pair per device, H2D / kernel / D2H
- * double-buffered), and the digests written back to host memory.
- * Synchronous.  offsets == NULL selects the fixed layout
+ * Host-memory batch, end to end: packets are read from host memory (DMA'd
+ * directly when the buffer is page-locked and the layout fixed, else staged
+ * through pinned buffers), hashed on every usable device (contiguous packet
+ * slices -- by bytes for the variable layout -- one host thread and stream
+ * pair per device, 64 MiB chunks double-buffered), and the digests stored
+ * by the kernels into page-locked host memory (the caller's buffer when it
+ * is page-locked).  Synchronous.  offsets == NULL selects the fixed layout
  * base[i * stride .. + fixed_len); otherwise packet i is
  * base[offsets[i] .. + lens[i]) and stride / fixed_len are ignored.
- * max_devices <= 0 uses every device; the device list starts at the
- * calling thread's current HIP device (so max_devices == 1 means "this
- * device" for a one-process-per-GPU caller).
+ * max_devices <= 0 uses every device, but no slice smaller than 16 MiB of
+ * payload (NET2_SHA2_SLICE_MIN_BYTES): a small batch stays on one device.
+ * The device list starts at the calling thread's current HIP device (so
+ * max_devices == 1 means "this device" for a one-process-per-GPU caller).
  */
 int net2_sha2_batch(int alg, const void *base, const uint64_t *offsets,
     const uint32_t *lens, uint64_t stride, uint32_t fixed_len, uint64_t n,

@@ -36,6 +36,8 @@ def dev():
 def virtual(monkeypatch):
     def set_k(k):
         monkeypatch.setenv("NET2_SHA2_VIRTUAL_DEVICES", str(k))
+        # test batches are small: slice them however small they are
+        monkeypatch.setenv("NET2_SHA2_SLICE_MIN_BYTES", "0")
     yield set_k
 
 
