@@ -658,7 +658,7 @@ def e2e_rate(steps, warmup, n=1 << 20, length=1024, ws=1, dev=None,
         ms = float(t[0])
     del host, outp
     return {"metric": "SHA-256 digests/s, 1 KiB packets from pinned host memory, "
-                      f"end to end (H2D + kernel + D2H), {ws} GPU(s)",
+                      f"end to end (H2D, kernel, digests stored to host memory), {ws} GPU(s)",
             "value": round(n * ws / (ms / 1e3), 1), "unit": "digests/s", "steps": steps,
             "n_gpus": ws, "ms_per_step": round(ms, 3),
             "workload": f"{ws} x 1M x 1 KiB, host -> GPU -> host via net2_sha2_batch, "
