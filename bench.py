@@ -678,7 +678,7 @@ def run_c1():
 
 
 def run_e2e(args, ws, rank, dev):
-    """Config 5 shape: host memory -> pinned H2D -> kernel -> D2H -> host,
+    """Config 5 shape: host memory -> pinned H2D -> kernel -> digests to host,
     through net2_sha2_batch on this rank's device (PCIe-inclusive rate)."""
     import torch
     import torch.distributed as dist
