@@ -117,10 +117,14 @@ struct Slot {
 };
 
 /*
- * zerocopy: the kernel reads the staging and writes the results through
- * the host mappings of coherent pinned buffers, so a batch costs one kernel
- * launch and no copy; otherwise staging is copied to device memory and the
- * results back.
+ * zerocopy (default): the kernel reads the staging through the host mapping
+ * of a coherent pinned buffer, so a batch costs one kernel launch and no
+ * copy; NET2_COALESCE_ZEROCOPY=0 copies the staging to device memory first.
+ * With the wave-per-job form the copy and its dependency cost more than
+ * the kernel's reads over PCIe: a lone 1 KiB call 48.5 against 51.1 us
+ * (SHA-512), 64 threads 385 k against 373 k calls/s (SHA-256: 453 k against
+ * 427 k), profiles/round2/coalesce_zc_ab.txt.  (Results always come back
+ * through coherent host memory written by the kernel.)
  */
 hipError_t host_alloc(uint8_t **p, size_t bytes, bool zerocopy)
 {
@@ -149,7 +153,7 @@ public:
 	    : nslots_(env_int("NET2_COALESCE_SLOTS", 4, 1, kMaxSlots)),
 	      window_(std::chrono::microseconds(
 		  env_int("NET2_COALESCE_WINDOW_US", 40, 0, 100000))),
-	      zerocopy_(env_int("NET2_COALESCE_ZEROCOPY", 0, 0, 1) != 0),
+	      zerocopy_(env_int("NET2_COALESCE_ZEROCOPY", 1, 0, 1) != 0),
 	      jobmode_(env_int("NET2_COALESCE_JOBMODE", 0, 0, 2))
 	{
 		for (int i = nslots_ - 1; i >= 0; i--)
