@@ -9,8 +9,10 @@
  *   - it launches at once if no other batch of this device is in flight
  *     (an idle GPU: lowest latency for a lone caller),
  *   - otherwise when the batch is full or the batching window (default
- *     40 us, NET2_COALESCE_WINDOW_US) has passed since it opened -- the
- *     callers that arrive while earlier batches run share one launch;
+ *     20 us, NET2_COALESCE_WINDOW_US) has passed since it opened -- the
+ *     callers that arrive while earlier batches run share one launch
+ *     (20 us measured best over 10 / 20 / 40 / 80 us at 8 and 64 threads,
+ *     profiles/round2/coalesce_window_ab.txt);
  * then it waits for the batch's event (spinning briefly, then blocking) and
  * hands every caller its result.  Several batches may be in flight at once
  * (NET2_COALESCE_SLOTS, default 4), each on its own stream.
@@ -152,7 +154,7 @@ public:
 	Coalescer()
 	    : nslots_(env_int("NET2_COALESCE_SLOTS", 4, 1, kMaxSlots)),
 	      window_(std::chrono::microseconds(
-		  env_int("NET2_COALESCE_WINDOW_US", 40, 0, 100000))),
+		  env_int("NET2_COALESCE_WINDOW_US", 20, 0, 100000))),
 	      zerocopy_(env_int("NET2_COALESCE_ZEROCOPY", 1, 0, 1) != 0),
 	      jobmode_(env_int("NET2_COALESCE_JOBMODE", 0, 0, 2))
 	{
