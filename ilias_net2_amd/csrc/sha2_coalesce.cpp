@@ -15,7 +15,8 @@
  *     profiles/round2/coalesce_window_ab.txt);
  * then it waits for the batch's event (spinning briefly, then blocking) and
  * hands every caller its result.  Several batches may be in flight at once
- * (NET2_COALESCE_SLOTS, default 4), each on its own stream.
+ * (NET2_COALESCE_SLOTS, default 8: ahead of 4 at 64 and 128 threads, even
+ * at 8, profiles/round2/coalesce_slots_ab.txt), each on its own stream.
  *
  * Layout of a batch in staging: every job's blocks (the message already
  * padded as SHA*Pad would, src/sha2.c:495-543 / :784-832, behind the
@@ -152,7 +153,7 @@ void futex_wake(std::atomic<int> *w)
 class Coalescer {
 public:
 	Coalescer()
-	    : nslots_(env_int("NET2_COALESCE_SLOTS", 4, 1, kMaxSlots)),
+	    : nslots_(env_int("NET2_COALESCE_SLOTS", 8, 1, kMaxSlots)),
 	      window_(std::chrono::microseconds(
 		  env_int("NET2_COALESCE_WINDOW_US", 20, 0, 100000))),
 	      zerocopy_(env_int("NET2_COALESCE_ZEROCOPY", 1, 0, 1) != 0),
