@@ -162,6 +162,18 @@ struct Sha512V : Sha512 {
 	static constexpr bool U2 = NET2_VAR512_PF != 0;
 	static constexpr bool PREFETCH = NET2_VAR512_PF != 0;
 };
+/* ... for the lane-per-job kernel of the coalescer (NET2_JOB512_PF, on),
+ * whose blocks come over PCIe from zero-copy staging: the next block's
+ * load is in flight while one is compressed (64 threads of 1 KiB SHA-512
+ * calls: 431 k against 399 k calls/s,
+ * profiles/round2/coalesce_job512_prefetch_ab.txt) ... */
+#ifndef NET2_JOB512_PF
+#define NET2_JOB512_PF 1
+#endif
+struct Sha512J : Sha512 {
+	static constexpr bool U2 = NET2_JOB512_PF != 0;
+	static constexpr bool PREFETCH = NET2_JOB512_PF != 0;
+};
 /* ... and for the variable-length HMAC kernels (NET2_HMAC512_PF) */
 #ifndef NET2_HMAC512_PF
 #define NET2_HMAC512_PF 0
@@ -1940,7 +1952,7 @@ hipError_t net2_launch_jobs(const uint8_t *stage, const Net2Job *jobs,
 		job_kernel<Sha256><<<(n256 + 63) / 64, 64, 0, s>>>(stage, jobs,
 		    n256, out, done);
 	if (n512 > 0)
-		job_kernel<Sha512><<<(n512 + 63) / 64, 64, 0, s>>>(stage,
+		job_kernel<Sha512J><<<(n512 + 63) / 64, 64, 0, s>>>(stage,
 		    jobs + n256, n512, out + 64 * (size_t)n256, done);
 	return hipGetLastError();
 }
