@@ -626,11 +626,58 @@ def extra_configs(args, dev, probe, ws=1, rank=0):
     return out
 
 
+def _parse_cpulist(text):
+    cpus = set()
+    for part in text.strip().split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            cpus.update(range(int(a), int(b) + 1))
+        elif part:
+            cpus.add(int(part))
+    return cpus
+
+
+def gpu_local_cpus(dev):
+    """CPUs of the NUMA node the GPU's PCIe link hangs off (sysfs), within
+    this process's affinity; None when unknown."""
+    import torch
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        bus = "%04x:%02x:%02x.0" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+        with open(f"/sys/bus/pci/devices/{bus}/numa_node") as f:
+            node = int(f.read())
+        if node < 0:
+            return None
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            cpus = _parse_cpulist(f.read()) & os.sched_getaffinity(0)
+        return cpus or None
+    except (OSError, ValueError):
+        return None
+
+
 def e2e_rate(steps, warmup, n=1 << 20, length=1024, ws=1, dev=None,
              dist_backend="nccl"):
     """C5's shape: 1 M x 1 KiB per GPU from pinned host memory -> the GPU ->
     digests back to pinned host memory, through net2_sha2_batch (each rank
     on its own GPU, max_devices 1); timed between barriers, max over ranks."""
+    import torch
+    import torch.distributed as dist
+    from ilias_net2_amd import _lib
+    # host buffers on the GPU's NUMA node (first touch by a thread running
+    # there), as a NUMA-aware caller would place them; affinity restored after
+    local = gpu_local_cpus(dev if dev is not None else torch.device("cuda", 0)) \
+        if os.environ.get("NET2_BENCH_NUMA", "1") != "0" else None
+    saved = os.sched_getaffinity(0)
+    if local:
+        os.sched_setaffinity(0, local)
+    try:
+        return _e2e_timed(steps, warmup, n, length, ws, dev, dist_backend,
+                          numa=bool(local))
+    finally:
+        os.sched_setaffinity(0, saved)
+
+
+def _e2e_timed(steps, warmup, n, length, ws, dev, dist_backend, numa):
     import torch
     import torch.distributed as dist
     from ilias_net2_amd import _lib
@@ -663,7 +710,8 @@ def e2e_rate(steps, warmup, n=1 << 20, length=1024, ws=1, dev=None,
             "n_gpus": ws, "ms_per_step": round(ms, 3),
             "workload": f"{ws} x 1M x 1 KiB, host -> GPU -> host via net2_sha2_batch, "
                         "one rank per GPU (BASELINE configs[4] at N=8)",
-            "h2d_GBps_per_gpu": round(n * length / (ms / 1e3) / 1e9, 2)}
+            "h2d_GBps_per_gpu": round(n * length / (ms / 1e3) / 1e9, 2),
+            "host_buffers_numa_local": numa}
 
 
 def run_c1():
