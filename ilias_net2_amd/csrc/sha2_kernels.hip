@@ -86,8 +86,11 @@ struct Sha256T {
 #ifndef NET2_HMAC_PAIR
 #define NET2_HMAC_PAIR 1
 #endif
+/* ordered asm rounds in the variable-length kernel: C3 452 against 463 us,
+ * {63, 511, 1499} B 481 against 494 us (round 2, three alternations,
+ * profiles/round2/var_asm_ab.txt) */
 #ifndef NET2_VAR_ASM
-#define NET2_VAR_ASM 0
+#define NET2_VAR_ASM 1
 #endif
 #ifndef NET2_VAR_U2
 #define NET2_VAR_U2 1

@@ -48,7 +48,7 @@ OUT = os.path.join(ROOT, "profiles", "isa_mix.json")
 KERNELS = {
     "c2": "_ZN4net23dev12fixed_kernelINS0_7Sha256TILb1ELb1ELb1EEELi0ELb1E",
     "c4": "_ZN4net23dev12fixed_kernelINS0_6Sha512ELi0ELb1E",
-    "c3": "_ZN4net23dev10var_kernelINS0_7Sha256TILb0ELb1ELb1EEE",
+    "c3": "_ZN4net23dev10var_kernelINS0_7Sha256TILb1ELb1ELb1EEE",
     "hmac": "_ZN4net23dev11hmac_kernelINS0_7Sha256TILb1ELb1ELb1EEELb1E",
     "hmac_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha256TILb1ELb1ELb1EEELb0ELi0E",
     "hmac512": "_ZN4net23dev11hmac_kernelINS0_6Sha512ELb1E",
