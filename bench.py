@@ -77,6 +77,7 @@ DLEN = {1: 32, 2: 48, 3: 64, 4: 32, 5: 48, 6: 64}
 ALG_NAMES = {1: "SHA-256", 2: "SHA-384", 3: "SHA-512", 4: "HMAC-SHA256",
              5: "HMAC-SHA384", 6: "HMAC-SHA512"}
 HMAC_KEY = bytes(range(64))
+EVENT_EVERY = 4     # event pair around every 4th timed step (kernel duration)
 
 
 def dist_env():
@@ -345,7 +346,8 @@ def device_step(name, inp, out, ws_buf, stream, unbinned=False):
 
 
 def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
-                       dist_backend="nccl", unbinned=False, clock_probe=None):
+                       dist_backend="nccl", unbinned=False, clock_probe=None,
+                       two_streams=False):
     """Untimed clock ramp and warmup, then exactly `steps` steps between
     barriers + synchronize; the dominant kernel's duration from HIP events
     on the launch stream.  Returns the measurements (max over ranks)."""
@@ -374,6 +376,17 @@ def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
         batch.hmac_sign_dev(alg, HMAC_KEY[:DLEN[alg]], inp["data"], inp["offs"],
                             inp["lens"], workspace=ws_buf)
     step = device_step(name, inp, out, ws_buf, stream, unbinned)
+    if two_streams:
+        # two batches in flight: odd steps on a second stream with their own
+        # digest buffer and workspace (the input batch is read-only)
+        stream2 = torch.cuda.Stream(dev)
+        out2 = torch.empty_like(out)
+        ws2 = torch.empty_like(ws_buf) if ws_buf is not None else None
+        step2 = device_step(name, inp, out2, ws2, stream2, unbinned)
+        step1 = step
+
+        def step_pair(k):
+            (step2 if k % 2 else step1)()
 
     # Clock ramp: repeat the step (untimed) for prewarm_ms of wall time.
     t_pw = time.perf_counter()
@@ -383,18 +396,40 @@ def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
     for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
+    if two_streams:
+        if ws > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(steps):
+            step_pair(k)
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+        del inp, out, ws_buf, out2, ws2
+        torch.cuda.empty_cache()
+        return {"ms_per_step": elapsed * 1e3 / steps, "steps": steps}
 
-    # HIP events on the stream the kernels are launched on.
+    # HIP events on the stream the kernels are launched on, around every
+    # EVENT_EVERY-th step: an event pair adds ~7 us of queue time to the step
+    # it brackets (profiles/round2/stream_events_ab.txt), so bracketing every
+    # step would bill that to the throughput; the sampled launches give the
+    # kernel duration.
+    sampled = [k % EVENT_EVERY == 0 for k in range(steps)]
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps)]
+          for _ in range(sum(sampled))]
     if ws > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for a, b in ev:
-        a.record(stream)
-        step()
-        b.record(stream)
+    j = 0
+    for k in range(steps):
+        if sampled[k]:
+            ev[j][0].record(stream)
+            step()
+            ev[j][1].record(stream)
+            j += 1
+        else:
+            step()
     # shader clock while the queued steps run, sampled every ~2 ms by a
     # helper thread (a sysfs read can take a millisecond: kept off the
     # thread whose synchronize ends the timed region)
@@ -417,7 +452,7 @@ def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
     if sampler:
         stop.set()
         sampler.join()
-    launch_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    launch_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
     if burst:   # every datagram of the synthetic burst is well-formed
         assert int((out != 0).sum()) == 0, f"{name}: datagrams not OK"
 
@@ -436,6 +471,7 @@ def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
         per_launch += n * (8 + 8 + DLEN[alg])
     res = {"n": n, "dlen": dlen, "payload": inp["payload"], "elapsed": elapsed,
            "ms_per_step": elapsed * 1e3 / steps, "launch_ms": launch_ms,
+           "event_pairs": len(ev),
            "per_launch_bytes": per_launch,
            "sclk_during_mhz": (round(sum(samples) / len(samples)) if samples else None),
            "sclk_samples": len(samples), "sclk_min_mhz": min(samples) if samples else None}
@@ -563,6 +599,7 @@ def main():
     value = r["n"] * ws / (r["ms_per_step"] / 1e3)
     roof, valu = rooflines(name, r["launch_ms"], r["per_launch_bytes"],
                            r["sclk_during_mhz"])
+    roof["event_pairs"] = r["event_pairs"]
     alg = cfg["alg"]
     line = {
         "metric": metric_of(name),
@@ -613,6 +650,7 @@ def extra_configs(args, dev, probe, ws=1, rank=0):
                                200.0, clock_probe=probe)
         roof, valu = rooflines(name, r["launch_ms"], r["per_launch_bytes"],
                            r["sclk_during_mhz"])
+        roof["event_pairs"] = r["event_pairs"]
         out[name] = {"metric": metric_of(name), "value": round(r["n"] / (r["ms_per_step"] / 1e3), 1),
                      "unit": unit_of(name), "steps": args.steps,
                      "ms_per_step": round(r["ms_per_step"], 4),
@@ -623,6 +661,20 @@ def extra_configs(args, dev, probe, ws=1, rank=0):
             out[name]["roofline_valu"] = valu
     out["e2e"] = e2e_rate(steps=10, warmup=3)
     out["c1"] = run_c1()
+    # Not the headline: the same steps issued alternately on two streams,
+    # two batches in flight, so one launch's tail overlaps the next one's
+    # head (and C3's binning the previous hash kernel); the rate a caller
+    # streaming batches through two streams gets.  No per-launch duration:
+    # the launches overlap.
+    two = {"note": "steps alternate over two streams, each with its own "
+                   "digest buffer and workspace; launches overlap"}
+    for name in ("c2", "c3", "c4"):
+        r = time_device_config(name, dev, args.steps, min(args.warmup, 10),
+                               200.0, two_streams=True)
+        two[name] = {"value": round(CONFIGS[name]["n"] / (r["ms_per_step"] / 1e3), 1),
+                     "unit": unit_of(name), "steps": r["steps"],
+                     "ms_per_step": round(r["ms_per_step"], 4)}
+    out["two_streams"] = two
     return out
 
 

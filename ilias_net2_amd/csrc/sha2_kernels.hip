@@ -319,6 +319,35 @@ __device__ __forceinline__ void materialize(const typename H::State &st)
 }
 
 /*
+ * NET2_PRIO=1 (A/B only, off): a wave's issue priority follows the work it
+ * has left (s_setprio 3..0 as its remaining blocks fall below 12 / 6 / 2),
+ * so that a draining grid's youngest waves -- those with the most blocks
+ * left, which the arbiter's age order serves last -- would not finish alone.
+ * Measured slower: C2 -5 %, C4 -6 %, C3 -1 % (profiles/round2/prio_ab.txt);
+ * the age order keeps the waves of a SIMD out of phase, so their loads do
+ * not all wait at once.
+ */
+#ifndef NET2_PRIO
+#define NET2_PRIO 0
+#endif
+__device__ __forceinline__ void prio_remaining(uint32_t rem_blocks)
+{
+#if NET2_PRIO
+	const uint32_t r = __builtin_amdgcn_readfirstlane(rem_blocks);
+	if (r >= 12)
+		__builtin_amdgcn_s_setprio(3);
+	else if (r >= 6)
+		__builtin_amdgcn_s_setprio(2);
+	else if (r >= 2)
+		__builtin_amdgcn_s_setprio(1);
+	else
+		__builtin_amdgcn_s_setprio(0);
+#else
+	(void)rem_blocks;
+#endif
+}
+
+/*
  * Whole-message digest for one lane.  nfull full blocks stream from p with
  * a one-block prefetch; then the generic tail (data remainder + 0x80 +
  * length, one or two blocks), or -- when the caller knows every message of
@@ -357,6 +386,7 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 		}
 		uint32_t q = 0;
 		for (; q + 2 <= npairs; q += 2) {
+			prio_remaining(nfull - 2 * q);
 			const uint8_t *bp = p + (size_t)q * 2 * H::BLOCK;
 			issue_block<NW32, AMODE>(bp + 2 * H::BLOCK, b0);
 			issue_block<NW32, AMODE>(bp + 3 * H::BLOCK, b1);
@@ -402,6 +432,7 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 			issue_block<NW32, AMODE>(p, ra);
 		uint32_t k = 0;
 		for (; k + 2 <= nfull; k += 2) {
+			prio_remaining(nfull - k);
 			const uint8_t *bp = p + (size_t)k * H::BLOCK;
 			issue_block<NW32, AMODE>(bp + H::BLOCK, rb);
 			uint32_t w[NW32];
@@ -429,6 +460,7 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 		if (nfull > 0)
 			issue_block<NW32, AMODE>(p, cur);
 		for (uint32_t k = 0; k < nfull; k++) {
+			prio_remaining(nfull - k);
 			const uint8_t *bp = p + (size_t)k * H::BLOCK;
 			Raw<NW32> nxt;
 			if (k + 1 < nfull)
@@ -440,6 +472,7 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 		}
 	} else {
 		for (uint32_t k = 0; k < nfull; k++) {
+			prio_remaining(nfull - k);
 			const uint8_t *bp = p + (size_t)k * H::BLOCK;
 			Raw<NW32> cur;
 			issue_block<NW32, AMODE>(bp, cur);
