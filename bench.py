@@ -209,6 +209,20 @@ def cpu_baseline(cfg):
     t0 = time.perf_counter()
     run(1, n1, True)
     single_u = n1 / (time.perf_counter() - t0)
+    # Context, not the baseline the north star names: the same batch through
+    # OpenSSL's SHA*_Init/Update/Final, the calls the reference's C++ layer
+    # makes (cxx_src/hash-openssl.cc:25-131; SHA-NI on this host's EPYC).
+    if cfg["kind"] == "fixed":
+        ossl = lambda t, m=n: oracle.openssl_batch(  # noqa: E731
+            alg, data, stride=cfg["length"], length=cfg["length"], n=m, nthreads=t)
+    else:
+        ossl = lambda t, m=n: oracle.openssl_batch(  # noqa: E731
+            alg, data, offsets=offs[:m], lens=lens[:m], nthreads=t)
+    t_ossl = _time_oracle(ossl, share)
+    ossl(1, n1)
+    t0 = time.perf_counter()
+    ossl(1, n1)
+    single_ossl = n1 / (time.perf_counter() - t0)
     what = cfg["workload"].split(" packets")[0]
     topo = _cpu_topology()
     # The headline is the best measured rate.  On the GPU boxes of this pool
@@ -242,6 +256,13 @@ def cpu_baseline(cfg):
                           "(an estimate, not a measurement; SMT not credited)"}
                 if phys else None),
             "single_thread_value": single,
+            "openssl_context": {
+                "value": n / t_ossl, "threads": share,
+                "single_thread_value": single_ossl,
+                "note": "not the src/sha2.c baseline: OpenSSL's SHA*_Init/"
+                        "Update/Final as the reference's C++ layer calls them "
+                        "(cxx_src/hash-openssl.cc:25-131), system libcrypto, "
+                        "its own SHA-NI / AVX2 transform; oracle/openssl_batch.c"},
             "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
             "affinity_cpus": affinity, "smt_active": _smt_active(), **topo}
 
@@ -346,8 +367,7 @@ def device_step(name, inp, out, ws_buf, stream, unbinned=False):
 
 
 def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
-                       dist_backend="nccl", unbinned=False, clock_probe=None,
-                       two_streams=False):
+                       dist_backend="nccl", unbinned=False, clock_probe=None):
     """Untimed clock ramp and warmup, then exactly `steps` steps between
     barriers + synchronize; the dominant kernel's duration from HIP events
     on the launch stream.  Returns the measurements (max over ranks)."""
@@ -376,18 +396,6 @@ def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
         batch.hmac_sign_dev(alg, HMAC_KEY[:DLEN[alg]], inp["data"], inp["offs"],
                             inp["lens"], workspace=ws_buf)
     step = device_step(name, inp, out, ws_buf, stream, unbinned)
-    if two_streams:
-        # two batches in flight: odd steps on a second stream with their own
-        # digest buffer and workspace (the input batch is read-only)
-        stream2 = torch.cuda.Stream(dev)
-        out2 = torch.empty_like(out)
-        ws2 = torch.empty_like(ws_buf) if ws_buf is not None else None
-        step2 = device_step(name, inp, out2, ws2, stream2, unbinned)
-        step1 = step
-
-        def step_pair(k):
-            (step2 if k % 2 else step1)()
-
     # Clock ramp: repeat the step (untimed) for prewarm_ms of wall time.
     t_pw = time.perf_counter()
     while (time.perf_counter() - t_pw) * 1e3 < prewarm_ms:
@@ -396,19 +404,6 @@ def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
     for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
-    if two_streams:
-        if ws > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for k in range(steps):
-            step_pair(k)
-        torch.cuda.synchronize(dev)
-        elapsed = time.perf_counter() - t0
-        del inp, out, ws_buf, out2, ws2
-        torch.cuda.empty_cache()
-        return {"ms_per_step": elapsed * 1e3 / steps, "steps": steps}
-
     # HIP events on the stream the kernels are launched on, around every
     # EVENT_EVERY-th step: an event pair adds ~7 us of queue time to the step
     # it brackets (profiles/round2/stream_events_ab.txt), so bracketing every
@@ -661,20 +656,6 @@ def extra_configs(args, dev, probe, ws=1, rank=0):
             out[name]["roofline_valu"] = valu
     out["e2e"] = e2e_rate(steps=10, warmup=3)
     out["c1"] = run_c1()
-    # Not the headline: the same steps issued alternately on two streams,
-    # two batches in flight, so one launch's tail overlaps the next one's
-    # head (and C3's binning the previous hash kernel); the rate a caller
-    # streaming batches through two streams gets.  No per-launch duration:
-    # the launches overlap.
-    two = {"note": "steps alternate over two streams, each with its own "
-                   "digest buffer and workspace; launches overlap"}
-    for name in ("c2", "c3", "c4"):
-        r = time_device_config(name, dev, args.steps, min(args.warmup, 10),
-                               200.0, two_streams=True)
-        two[name] = {"value": round(CONFIGS[name]["n"] / (r["ms_per_step"] / 1e3), 1),
-                     "unit": unit_of(name), "steps": r["steps"],
-                     "ms_per_step": round(r["ms_per_step"], 4)}
-    out["two_streams"] = two
     return out
 
 

@@ -103,6 +103,37 @@ def batch(alg: int, data: np.ndarray, offsets=None, lens=None, stride=0,
     return out
 
 
+_ossl = None
+
+
+def openssl_batch(alg: int, data: np.ndarray, offsets=None, lens=None,
+                  stride=0, length=0, n=None, nthreads=1) -> np.ndarray:
+    """The same batch through OpenSSL's SHA*_Init/Update/Final, the calls
+    the reference's C++ layer makes (cxx_src/hash-openssl.cc:25-131); a CPU
+    baseline for context (oracle/openssl_batch.c)."""
+    global _ossl
+    if _ossl is None:
+        path = os.path.join(HERE, "libcpu_openssl.so")
+        if not os.path.exists(path):
+            build()
+        _ossl = ctypes.CDLL(path)
+        _ossl.cpu_openssl_batch.restype = ctypes.c_int
+        _ossl.cpu_openssl_batch.argtypes = [
+            ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_uint64, ctypes.c_uint32, ctypes.c_size_t, ctypes.c_void_p,
+            ctypes.c_int]
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    if offsets is not None:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        n = len(offsets)
+    out = np.empty((n, DIGEST_LEN[alg]), dtype=np.uint8)
+    if _ossl.cpu_openssl_batch(alg, _ptr(data), _ptr(offsets), _ptr(lens),
+                               stride, length, n, _ptr(out), nthreads) != 0:
+        raise ValueError(f"bad alg {alg}")
+    return out
+
+
 def ph_to_iv(seq: int, flags: int, ivlen: int) -> bytes:
     out = ctypes.create_string_buffer(max(ivlen, 1))
     lib().oracle_ph_to_iv(seq, flags, ivlen, out)

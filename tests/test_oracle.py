@@ -133,6 +133,23 @@ def test_unrolled_variant(oracle_mod, golden):
             assert d[i].tobytes() == h(m).digest(), (alg, i)
 
 
+def test_openssl_context_baseline(oracle_mod, golden):
+    """The OpenSSL leg of bench.py's cpu_baseline (oracle/openssl_batch.c,
+    SHA*_Init/Update/Final as cxx_src/hash-openssl.cc calls them) hashes
+    the golden batches to the same digests."""
+    for b in golden["batches"]:
+        if b["kind"] == "fixed":
+            data = synth.fixed_batch(b["seed"], b["n"], b["len"], b["stride"])
+            d = oracle_mod.openssl_batch(b["alg"], data, stride=b["stride"],
+                                         length=b["len"], n=b["n"], nthreads=3)
+        else:
+            lens = synth.mixed_lengths(b["len_seed"], b["n"])
+            data, offs = synth.packed(b["seed"], lens, align=b["align"])
+            d = oracle_mod.openssl_batch(b["alg"], data, offsets=offs,
+                                         lens=lens, nthreads=2)
+        assert hashlib.sha256(d.tobytes()).hexdigest() == b["digest_of_digests"]
+
+
 def _ctx_digest(L, pfx, chunks, dl):
     ctx = ctypes.create_string_buffer(208)
     getattr(L, f"oracle_{pfx}_init")(ctx)
