@@ -44,6 +44,7 @@ struct Sha256T {
 	static constexpr bool ASM = ASM_;
 	static constexpr bool U2 = U2_;
 	static constexpr bool PAIR = PAIR_;
+	static constexpr bool DRAIN = false;
 	typedef uint32_t word;
 	static constexpr int BLOCK = 64;	/* bytes per block */
 	static constexpr int NW32 = 16;		/* 32-bit words per block */
@@ -117,10 +118,16 @@ typedef Sha256T<NET2_ASM256 != 0, NET2_ABSORB_U2 != 0, NET2_FIXED_PAIR != 0> Sha
 typedef Sha256T<NET2_VAR_ASM != 0, NET2_VAR_U2 != 0, NET2_VAR_PAIR != 0> Sha256V;	/* var */
 typedef Sha256T<NET2_HMAC_ASM != 0, NET2_HMAC_U2 != 0, NET2_HMAC_PAIR != 0> Sha256H;	/* HMAC */
 
+/* drain priority in the fixed SHA-512 kernel (prio_remaining below) */
+#ifndef NET2_SHA512_DRAIN
+#define NET2_SHA512_DRAIN 1
+#endif
 struct Sha512 {
 	static constexpr bool ASM = false;
 	static constexpr bool U2 = false;	/* no prefetch: nothing to ping-pong */
 	static constexpr bool PAIR = false;	/* a 128-byte block is a whole line */
+	/* drain priority (prio_remaining): the fixed kernel only */
+	static constexpr bool DRAIN = NET2_SHA512_DRAIN != 0;
 	typedef uint64_t word;
 	static constexpr int BLOCK = 128;
 	static constexpr int NW32 = 32;
@@ -162,6 +169,7 @@ struct Sha512 {
 #define NET2_VAR512_PF 0
 #endif
 struct Sha512V : Sha512 {
+	static constexpr bool DRAIN = false;
 	static constexpr bool U2 = NET2_VAR512_PF != 0;
 	static constexpr bool PREFETCH = NET2_VAR512_PF != 0;
 };
@@ -174,6 +182,7 @@ struct Sha512V : Sha512 {
 #define NET2_JOB512_PF 1
 #endif
 struct Sha512J : Sha512 {
+	static constexpr bool DRAIN = false;
 	static constexpr bool U2 = NET2_JOB512_PF != 0;
 	static constexpr bool PREFETCH = NET2_JOB512_PF != 0;
 };
@@ -182,6 +191,7 @@ struct Sha512J : Sha512 {
 #define NET2_HMAC512_PF 0
 #endif
 struct Sha512H : Sha512 {
+	static constexpr bool DRAIN = false;
 	static constexpr bool U2 = NET2_HMAC512_PF != 0;
 	static constexpr bool PREFETCH = NET2_HMAC512_PF != 0;
 };
@@ -319,20 +329,37 @@ __device__ __forceinline__ void materialize(const typename H::State &st)
 }
 
 /*
- * NET2_PRIO=1 (A/B only, off): a wave's issue priority follows the work it
- * has left (s_setprio 3..0 as its remaining blocks fall below 12 / 6 / 2),
- * so that a draining grid's youngest waves -- those with the most blocks
- * left, which the arbiter's age order serves last -- would not finish alone.
- * Measured slower: C2 -5 %, C4 -6 %, C3 -1 % (profiles/round2/prio_ab.txt);
- * the age order keeps the waves of a SIMD out of phase, so their loads do
- * not all wait at once.
+ * Issue priority while a grid drains (H::DRAIN: the fixed SHA-512 kernel).
+ * The SIMD's VALU arbiter serves the oldest wave first, so when the grid's
+ * last generation of waves is dispatched, the youngest waves -- those with
+ * the most blocks left -- progress last and finish alone, at one wave's
+ * issue rate.  In the workgroups of the grid's last NET2_PRIO_GEN x 256 (two
+ * per CU), a wave's priority follows the work it has left (s_setprio 3..0
+ * as its remaining blocks fall below 12 / 6 / 2), so the waves of a SIMD
+ * end closer together.  C4 +1.0 % (six alternations on two boxes; one or
+ * three / four generations: +0.7 % / flat), C2 flat
+ * (profiles/round2/drain_prio_ab.txt).
+ *
+ * NET2_PRIO (A/B only) overrides it for every kernel: 1 = the same
+ * priority in every wave of the grid -- slower, C2 -5 %, C4 -6 %, C3 -1 %
+ * (profiles/round2/prio_ab.txt): the age order keeps the waves of a SIMD out
+ * of phase, so their loads do not all wait at once; 2 = drain-only.
  */
 #ifndef NET2_PRIO
 #define NET2_PRIO 0
 #endif
+#ifndef NET2_PRIO_GEN
+#define NET2_PRIO_GEN 2
+#endif
+template <bool DRAIN>
 __device__ __forceinline__ void prio_remaining(uint32_t rem_blocks)
 {
-#if NET2_PRIO
+	constexpr int mode = NET2_PRIO ? NET2_PRIO : DRAIN ? 2 : 0;
+	if (mode == 0)
+		return;
+	if (mode == 2 && (gridDim.x < 4 * 256 * NET2_PRIO_GEN ||
+	    blockIdx.x + 256 * NET2_PRIO_GEN < gridDim.x))
+		return;
 	const uint32_t r = __builtin_amdgcn_readfirstlane(rem_blocks);
 	if (r >= 12)
 		__builtin_amdgcn_s_setprio(3);
@@ -342,9 +369,6 @@ __device__ __forceinline__ void prio_remaining(uint32_t rem_blocks)
 		__builtin_amdgcn_s_setprio(1);
 	else
 		__builtin_amdgcn_s_setprio(0);
-#else
-	(void)rem_blocks;
-#endif
 }
 
 /*
@@ -386,7 +410,7 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 		}
 		uint32_t q = 0;
 		for (; q + 2 <= npairs; q += 2) {
-			prio_remaining(nfull - 2 * q);
+			prio_remaining<H::DRAIN>(nfull - 2 * q);
 			const uint8_t *bp = p + (size_t)q * 2 * H::BLOCK;
 			issue_block<NW32, AMODE>(bp + 2 * H::BLOCK, b0);
 			issue_block<NW32, AMODE>(bp + 3 * H::BLOCK, b1);
@@ -432,7 +456,7 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 			issue_block<NW32, AMODE>(p, ra);
 		uint32_t k = 0;
 		for (; k + 2 <= nfull; k += 2) {
-			prio_remaining(nfull - k);
+			prio_remaining<H::DRAIN>(nfull - k);
 			const uint8_t *bp = p + (size_t)k * H::BLOCK;
 			issue_block<NW32, AMODE>(bp + H::BLOCK, rb);
 			uint32_t w[NW32];
@@ -460,7 +484,7 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 		if (nfull > 0)
 			issue_block<NW32, AMODE>(p, cur);
 		for (uint32_t k = 0; k < nfull; k++) {
-			prio_remaining(nfull - k);
+			prio_remaining<H::DRAIN>(nfull - k);
 			const uint8_t *bp = p + (size_t)k * H::BLOCK;
 			Raw<NW32> nxt;
 			if (k + 1 < nfull)
@@ -472,7 +496,7 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 		}
 	} else {
 		for (uint32_t k = 0; k < nfull; k++) {
-			prio_remaining(nfull - k);
+			prio_remaining<H::DRAIN>(nfull - k);
 			const uint8_t *bp = p + (size_t)k * H::BLOCK;
 			Raw<NW32> cur;
 			issue_block<NW32, AMODE>(bp, cur);
