@@ -39,12 +39,12 @@ namespace dev {
  *   PAIR: the pair loop -- both 64-byte blocks of a 128-byte line requested
  *         together, one pair ahead (absorb below).
  */
-template <bool ASM_, bool U2_, bool PAIR_ = false>
+template <bool ASM_, bool U2_, bool PAIR_ = false, bool DRAIN_ = false>
 struct Sha256T {
 	static constexpr bool ASM = ASM_;
 	static constexpr bool U2 = U2_;
 	static constexpr bool PAIR = PAIR_;
-	static constexpr bool DRAIN = false;
+	static constexpr bool DRAIN = DRAIN_;	/* prio_remaining */
 	typedef uint32_t word;
 	static constexpr int BLOCK = 64;	/* bytes per block */
 	static constexpr int NW32 = 16;		/* 32-bit words per block */
@@ -115,7 +115,14 @@ typedef Sha256T<NET2_ASM256 != 0, NET2_ABSORB_U2 != 0, NET2_FIXED_PAIR != 0> Sha
 #ifndef NET2_VAR_PAIR
 #define NET2_VAR_PAIR 1
 #endif
-typedef Sha256T<NET2_VAR_ASM != 0, NET2_VAR_U2 != 0, NET2_VAR_PAIR != 0> Sha256V;	/* var */
+/* drain priority (prio_remaining) in the variable-length kernel: A/B only,
+ * off -- C3 +1.4 %, the byte-aligned mix -0.6 %
+ * (profiles/round2/var_drain_ab.txt) */
+#ifndef NET2_VAR256_DRAIN
+#define NET2_VAR256_DRAIN 0
+#endif
+typedef Sha256T<NET2_VAR_ASM != 0, NET2_VAR_U2 != 0, NET2_VAR_PAIR != 0,
+    NET2_VAR256_DRAIN != 0> Sha256V;	/* var */
 typedef Sha256T<NET2_HMAC_ASM != 0, NET2_HMAC_U2 != 0, NET2_HMAC_PAIR != 0> Sha256H;	/* HMAC */
 
 /* drain priority in the fixed SHA-512 kernel (prio_remaining below) */
