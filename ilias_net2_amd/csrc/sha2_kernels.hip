@@ -929,7 +929,45 @@ __device__ __forceinline__ void hmac_lane(const uint8_t *p, uint32_t len,
  *                 message (the net2_buffer_cmp of :254), 1 if it does not,
  *                 2 if the datagram is shorter than dlen (:240-244).
  */
-enum { HMAC_DIGESTS = 0, HMAC_SIGN = 1, HMAC_VERIFY = 2 };
+enum { HMAC_DIGESTS = 0, HMAC_SIGN = 1, HMAC_VERIFY = 2, HMAC_BURST_RX = 3,
+    HMAC_BURST_TX = 4 };
+
+/*
+ * Packet-burst codes (the burst kernels below): the status byte is the
+ * NET2_P{EN,DE}CODE_* code, | BURST_VERIFY when the HMAC verdict of the
+ * datagram's region decides it.
+ */
+#define BURST_VERIFY 0x80u
+#define PKT_PH_ENCRYPTED 0x00000001u	/* types/packet.n2t:27 */
+#define PKT_PH_SIGNED 0x00000002u	/* types/packet.n2t:28 */
+#define PKT_OK 0
+#define PKT_RESOURCE 1
+#define PKT_BAD 2
+#define PKT_UNSAFE 3
+
+__device__ __forceinline__ uint32_t load_be32_bytes(const uint8_t *p)
+{
+	return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) |
+	    ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+
+/*
+ * HMAC_BURST_RX: the per-datagram bookkeeping of net2_packet_decode folded
+ * into the VERIFY kernel.  offsets / lens describe whole wire datagrams;
+ * each lane decodes its datagram's header (cp_packet_header,
+ * types/packet.n2t:196-198), checks the flags against the negotiated keys
+ * (:217-221; a hash key is always set on this path), and, when PH_SIGNED,
+ * verifies "hash field || payload" after the 8-byte header (:233-257) --
+ * exactly burst_prep_kernel's RX branch followed by HMAC_VERIFY, without
+ * prep's extra pass over every datagram's first line.  Writes the status
+ * (| BURST_VERIFY), seq and flags per datagram and the verdict to out.
+ * HMAC_BURST_TX: the same for net2_packet_encode (out == base): the lane
+ * takes seq / flags from the caller's arrays, applies the encode-side flag
+ * checks (:364-370) and the room check, writes the header (:384-392) and
+ * signs the payload into the hash field (:410-427), as burst_prep_kernel's
+ * TX branch followed by HMAC_SIGN; status per datagram.
+ */
+/* (struct BurstRx: sha2_launch.h) */
 
 /* VERIFY: compare the hash field in whole words when the wave's message
  * starts (and so its hash fields) are 4- or 16-byte aligned */
@@ -942,7 +980,7 @@ __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ b
     const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
     const uint32_t *__restrict__ perm, uint64_t stride, uint32_t fixed_len,
     uint64_t n, uint8_t *__restrict__ out, uint32_t dlen, int is384,
-    HKey<H::NW32> key, PadKW<typename H::word> pad)
+    HKey<H::NW32> key, PadKW<typename H::word> pad, BurstRx rx)
 {
 	constexpr int NW32 = H::NW32;
 	__shared__ uint32_t mid[2][16];
@@ -986,6 +1024,51 @@ __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ b
 		p = base + (live ? i * stride : 0);
 		len = live ? fixed_len : 0;
 	}
+	uint32_t rx_st = PKT_OK, rx_seq = 0, rx_fl = 0;
+	if (MODE == HMAC_BURST_TX) {
+		if (live) {
+			rx_seq = rx.seq[i];
+			rx_fl = rx.flags[i];
+		}
+		const bool sg = (rx_fl & PKT_PH_SIGNED) != 0;
+		const bool cr = (rx_fl & PKT_PH_ENCRYPTED) != 0;
+		if (!sg || cr != (rx.enc_set != 0))
+			rx_st = PKT_UNSAFE;
+		else if (len < 8 + dlen)
+			rx_st = PKT_RESOURCE;	/* no room for header and hash */
+		if (live && rx_st == PKT_OK) {
+			uint8_t *h = out + (p - base);
+#pragma unroll
+			for (int b = 0; b < 4; b++) {
+				h[b] = (uint8_t)(rx_seq >> (24 - 8 * b));
+				h[4 + b] = (uint8_t)(rx_fl >> (24 - 8 * b));
+			}
+			p += 8;
+			len -= 8;
+		} else {
+			len = 0;
+		}
+		if (live)
+			rx.status[i] = (uint8_t)rx_st;
+	}
+	if (MODE == HMAC_BURST_RX) {
+		if (len < 8) {
+			rx_st = PKT_BAD;	/* header decode fails */
+		} else {
+			rx_seq = load_be32_bytes(p);
+			rx_fl = load_be32_bytes(p + 4);
+		}
+		if (rx_st == PKT_OK && ((rx_fl & PKT_PH_SIGNED) == 0 ||
+		    (rx.enc_set && (rx_fl & PKT_PH_ENCRYPTED) == 0)))
+			rx_st = PKT_UNSAFE;
+		if (rx_st == PKT_OK) {
+			rx_st |= BURST_VERIFY;	/* hash field || payload */
+			p += 8;
+			len -= 8;
+		} else {
+			len = 0;
+		}
+	}
 	const uint8_t *field = p;	/* SIGN / VERIFY: the hash field */
 	const bool short_dgram = MODE != HMAC_DIGESTS && len < dlen;
 	if (MODE != HMAC_DIGESTS) {
@@ -1017,7 +1100,7 @@ __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ b
 		return;
 	uint32_t o[16];
 	H::out_words(st, o, is384);
-	if (MODE == HMAC_VERIFY) {
+	if (MODE == HMAC_VERIFY || MODE == HMAC_BURST_RX) {
 		/* o[] holds the digest bytes little-endian per word, the order
 		 * store_digest writes them in */
 		uint32_t diff = 0;
@@ -1049,10 +1132,16 @@ __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ b
 					    ((o[j >> 2] >> (8 * (j & 3))) & 0xffu);
 		}
 		out[i] = short_dgram ? 2 : diff != 0;
+		if (MODE == HMAC_BURST_RX) {
+			rx.status[i] = (uint8_t)rx_st;
+			rx.seq[i] = rx_seq;
+			rx.flags[i] = rx_fl;
+		}
 		return;
 	}
-	uint8_t *dst = MODE == HMAC_SIGN ? out + (field - base) : out + i * dlen;
-	if (MODE == HMAC_SIGN && short_dgram)
+	constexpr bool SIGNS = MODE == HMAC_SIGN || MODE == HMAC_BURST_TX;
+	uint8_t *dst = SIGNS ? out + (field - base) : out + i * dlen;
+	if (SIGNS && short_dgram)
 		return;
 	if (dlen == 48)
 		store_digest<48>(dst, o);
@@ -1370,19 +1459,7 @@ __global__ __launch_bounds__(256) void ph_iv_kernel(const uint32_t *__restrict__
  * status byte: the NET2_P{EN,DE}CODE_* code, | BURST_VERIFY when the HMAC
  * verdict of the region decides it.
  */
-#define BURST_VERIFY 0x80u
-#define PKT_PH_ENCRYPTED 0x00000001u	/* types/packet.n2t:27 */
-#define PKT_PH_SIGNED 0x00000002u	/* types/packet.n2t:28 */
-#define PKT_OK 0
-#define PKT_RESOURCE 1
-#define PKT_BAD 2
-#define PKT_UNSAFE 3
-
-__device__ __forceinline__ uint32_t load_be32_bytes(const uint8_t *p)
-{
-	return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) |
-	    ((uint32_t)p[2] << 8) | (uint32_t)p[3];
-}
+/* (BURST_VERIFY, the PKT_* codes and load_be32_bytes: above hmac_kernel) */
 
 __global__ __launch_bounds__(256) void burst_prep_kernel(uint8_t *__restrict__ base,
     const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
@@ -1920,27 +1997,38 @@ template <class H>
 static void launch_hmac_var_mode(int mode, unsigned grid, hipStream_t s,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
     const uint32_t *perm, uint64_t n, uint8_t *out, uint32_t dlen, int is384,
-    HKey<H::NW32> k, PadKW<typename H::word> pad)
+    HKey<H::NW32> k, PadKW<typename H::word> pad, BurstRx rx)
 {
 	if (mode == HMAC_SIGN)
 		hmac_kernel<H, false, HMAC_SIGN><<<grid, 256, 0, s>>>(base, offsets,
-		    lens, perm, 0, 0, n, out, dlen, is384, k, pad);
+		    lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx);
 	else if (mode == HMAC_VERIFY)
 		hmac_kernel<typename NoPair<H>::type, false, HMAC_VERIFY>
 		    <<<grid, 256, 0, s>>>(base, offsets, lens, perm, 0, 0, n, out,
-		    dlen, is384, k, pad);
+		    dlen, is384, k, pad, rx);
+	else if (mode == HMAC_BURST_RX)
+		hmac_kernel<typename NoPair<H>::type, false, HMAC_BURST_RX>
+		    <<<grid, 256, 0, s>>>(base, offsets, lens, perm, 0, 0, n, out,
+		    dlen, is384, k, pad, rx);
+	else if (mode == HMAC_BURST_TX)
+		hmac_kernel<H, false, HMAC_BURST_TX><<<grid, 256, 0, s>>>(base,
+		    offsets, lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx);
 	else
 		hmac_kernel<H, false><<<grid, 256, 0, s>>>(base, offsets,
-		    lens, perm, 0, 0, n, out, dlen, is384, k, pad);
+		    lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx);
 }
 
 hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
     uint64_t stride, uint32_t fixed_len, uint64_t n, uint8_t *out,
-    uint32_t *ws, hipStream_t s, int mode)
+    uint32_t *ws, hipStream_t s, int mode, const BurstRx *burst_rx)
 {
 	if (mode != HMAC_DIGESTS && offsets == nullptr)
 		return hipErrorInvalidValue;	/* datagram modes: var layout */
+	if ((mode == HMAC_BURST_RX || mode == HMAC_BURST_TX) !=
+	    (burst_rx != nullptr))
+		return hipErrorInvalidValue;
+	const BurstRx rx = burst_rx ? *burst_rx : BurstRx{};
 	if (n == 0)
 		return hipSuccess;
 	const int halg = alg - 3;	/* HMAC row -> SHA row */
@@ -1972,13 +2060,13 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 		if (padconst) {
 			pad_kw256(ibits, pad);
 			hmac_kernel<Sha256H, true><<<grid, 256, 0, s>>>(base, offsets,
-			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad);
+			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad, rx);
 		} else if (offsets != nullptr) {
 			launch_hmac_var_mode<Sha256H>(mode, grid, s, base, offsets,
-			    lens, perm, n, out, dlen, 0, k, pad);
+			    lens, perm, n, out, dlen, 0, k, pad, rx);
 		} else {
 			hmac_kernel<Sha256H, false><<<grid, 256, 0, s>>>(base, offsets,
-			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad);
+			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad, rx);
 		}
 	} else {
 		HKey<32> k;
@@ -1989,13 +2077,13 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 		if (padconst) {
 			pad_kw512(ibits, pad);
 			hmac_kernel<Sha512, true><<<grid, 256, 0, s>>>(base, offsets,
-			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad);
+			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad, rx);
 		} else if (offsets != nullptr) {
 			launch_hmac_var_mode<Sha512H>(mode, grid, s, base, offsets,
-			    lens, perm, n, out, dlen, is384, k, pad);
+			    lens, perm, n, out, dlen, is384, k, pad, rx);
 		} else {
 			hmac_kernel<Sha512, false><<<grid, 256, 0, s>>>(base, offsets,
-			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad);
+			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad, rx);
 		}
 	}
 	return hipGetLastError();

@@ -47,10 +47,32 @@ hipError_t net2_bin_order(int alg, const uint32_t *lens, uint64_t n,
 #define NET2_HMAC_MODE_DIGESTS 0
 #define NET2_HMAC_MODE_SIGN 1
 #define NET2_HMAC_MODE_VERIFY 2
+/*
+ * 3: the RX burst (net2_packet_decode_burst with a hash key): offsets /
+ * lens are whole wire datagrams; each lane decodes the 8-byte header, sets
+ * status (NET2_PDECODE_* | 0x80 when the verdict decides), seq and flags,
+ * and verifies "hash field || payload" after the header into out[i] as in
+ * mode 2.  Requires burst_rx.
+ */
+#define NET2_HMAC_MODE_BURST_RX 3
+/*
+ * 4: the TX burst (net2_packet_encode_burst with a hash key, out = base):
+ * seq / flags are the caller's per-datagram inputs; each lane checks the
+ * flags and the room, writes the 8-byte header, signs the payload into the
+ * hash field after it and sets status.  Requires burst_rx.
+ */
+#define NET2_HMAC_MODE_BURST_TX 4
+struct BurstRx {
+	uint32_t *seq;		/* RX: out; TX: in */
+	uint32_t *flags;	/* RX: out; TX: in */
+	uint8_t *status;
+	int enc_set;
+};
 hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
     uint64_t stride, uint32_t fixed_len, uint64_t n, uint8_t *out,
-    uint32_t *ws, hipStream_t s, int mode = NET2_HMAC_MODE_DIGESTS);
+    uint32_t *ws, hipStream_t s, int mode = NET2_HMAC_MODE_DIGESTS,
+    const BurstRx *burst_rx = nullptr);
 
 /*
  * Coalesced small jobs (sha2_coalesce.cpp): many independent requests from

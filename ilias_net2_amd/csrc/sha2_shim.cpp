@@ -1108,13 +1108,18 @@ NET2_EXPORT int net2_packet_decode_burst(int hash_alg, const void *hash_key,
 	uint32_t *seq = d_seq ? d_seq : w.seq, *flags = d_flags ? d_flags : w.flags;
 	hipStream_t s = (hipStream_t)stream;
 	const int hash_set = hash_alg != NET2_HASH_NIL;
-	HIP_TRY(net2_launch_burst_prep((uint8_t *)d_base, d_offsets, d_lens, n,
-	    0, hash_set, enc_alg != 0, hash_set ? kRows[hash_alg].hashlen : 0,
-	    nullptr, nullptr, seq, flags, w.sub_off, w.sub_len, w.status, s));
-	if (hash_set)
+	if (hash_set) {
+		/* header decode, flag checks and HMAC verify in one kernel over
+		 * the wire datagrams (binned by datagram length) */
+		const BurstRx rx = { seq, flags, w.status, enc_alg != 0 };
 		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)hash_key,
-		    hash_keylen, (const uint8_t *)d_base, w.sub_off, w.sub_len, 0,
-		    0, n, w.verdict, w.bin, s, NET2_HMAC_MODE_VERIFY));
+		    hash_keylen, (const uint8_t *)d_base, d_offsets, d_lens, 0,
+		    0, n, w.verdict, w.bin, s, NET2_HMAC_MODE_BURST_RX, &rx));
+	} else {
+		HIP_TRY(net2_launch_burst_prep((uint8_t *)d_base, d_offsets,
+		    d_lens, n, 0, 0, enc_alg != 0, 0, nullptr, nullptr, seq,
+		    flags, w.sub_off, w.sub_len, w.status, s));
+	}
 	HIP_TRY(net2_launch_burst_final(n, w.status, w.verdict, seq, flags,
 	    enc_alg != 0 ? ivlen : 0, (uint8_t *)d_iv, d_result, s));
 	return 0;
@@ -1136,13 +1141,20 @@ NET2_EXPORT int net2_packet_encode_burst(int hash_alg, const void *hash_key,
 	burst_layout(n, (uint8_t *)d_ws, &w);
 	hipStream_t s = (hipStream_t)stream;
 	const int hash_set = hash_alg != NET2_HASH_NIL;
-	HIP_TRY(net2_launch_burst_prep((uint8_t *)d_base, d_offsets, d_lens, n,
-	    1, hash_set, enc_alg != 0, hash_set ? kRows[hash_alg].hashlen : 0,
-	    d_seq, d_flags, nullptr, nullptr, w.sub_off, w.sub_len, w.status, s));
-	if (hash_set)
+	if (hash_set) {
+		/* flag and room checks, header write and HMAC sign in one
+		 * kernel over the wire datagrams */
+		const BurstRx tx = { const_cast<uint32_t *>(d_seq),
+		    const_cast<uint32_t *>(d_flags), w.status, enc_alg != 0 };
 		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)hash_key,
-		    hash_keylen, (const uint8_t *)d_base, w.sub_off, w.sub_len, 0,
-		    0, n, (uint8_t *)d_base, w.bin, s, NET2_HMAC_MODE_SIGN));
+		    hash_keylen, (const uint8_t *)d_base, d_offsets, d_lens, 0,
+		    0, n, (uint8_t *)d_base, w.bin, s, NET2_HMAC_MODE_BURST_TX,
+		    &tx));
+	} else {
+		HIP_TRY(net2_launch_burst_prep((uint8_t *)d_base, d_offsets,
+		    d_lens, n, 1, 0, enc_alg != 0, 0, d_seq, d_flags, nullptr,
+		    nullptr, w.sub_off, w.sub_len, w.status, s));
+	}
 	HIP_TRY(net2_launch_burst_final(n, w.status, nullptr, d_seq, d_flags, 0,
 	    nullptr, d_result, s));
 	return 0;
