@@ -1143,13 +1143,15 @@ NET2_EXPORT int net2_packet_encode_burst(int hash_alg, const void *hash_key,
 	const int hash_set = hash_alg != NET2_HASH_NIL;
 	if (hash_set) {
 		/* flag and room checks, header write and HMAC sign in one
-		 * kernel over the wire datagrams */
+		 * kernel over the wire datagrams; the TX code is final (no
+		 * verdict to fold in), so the kernel writes it to d_result */
 		const BurstRx tx = { const_cast<uint32_t *>(d_seq),
-		    const_cast<uint32_t *>(d_flags), w.status, enc_alg != 0 };
+		    const_cast<uint32_t *>(d_flags), d_result, enc_alg != 0 };
 		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)hash_key,
 		    hash_keylen, (const uint8_t *)d_base, d_offsets, d_lens, 0,
 		    0, n, (uint8_t *)d_base, w.bin, s, NET2_HMAC_MODE_BURST_TX,
 		    &tx));
+		return 0;
 	} else {
 		HIP_TRY(net2_launch_burst_prep((uint8_t *)d_base, d_offsets,
 		    d_lens, n, 1, 0, enc_alg != 0, 0, d_seq, d_flags, nullptr,
