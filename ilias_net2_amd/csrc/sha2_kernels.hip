@@ -967,7 +967,7 @@ __device__ __forceinline__ uint32_t load_be32_bytes(const uint8_t *p)
  * signs the payload into the hash field (:410-427), as burst_prep_kernel's
  * TX branch followed by HMAC_SIGN; status per datagram.
  */
-/* (struct BurstRx: sha2_launch.h) */
+/* (struct BurstArgs: sha2_launch.h) */
 
 /* VERIFY: compare the hash field in whole words when the wave's message
  * starts (and so its hash fields) are 4- or 16-byte aligned */
@@ -980,7 +980,7 @@ __global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ b
     const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
     const uint32_t *__restrict__ perm, uint64_t stride, uint32_t fixed_len,
     uint64_t n, uint8_t *__restrict__ out, uint32_t dlen, int is384,
-    HKey<H::NW32> key, PadKW<typename H::word> pad, BurstRx rx)
+    HKey<H::NW32> key, PadKW<typename H::word> pad, BurstArgs rx)
 {
 	constexpr int NW32 = H::NW32;
 	__shared__ uint32_t mid[2][16];
@@ -1997,7 +1997,7 @@ template <class H>
 static void launch_hmac_var_mode(int mode, unsigned grid, hipStream_t s,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
     const uint32_t *perm, uint64_t n, uint8_t *out, uint32_t dlen, int is384,
-    HKey<H::NW32> k, PadKW<typename H::word> pad, BurstRx rx)
+    HKey<H::NW32> k, PadKW<typename H::word> pad, BurstArgs rx)
 {
 	if (mode == HMAC_SIGN)
 		hmac_kernel<H, false, HMAC_SIGN><<<grid, 256, 0, s>>>(base, offsets,
@@ -2021,14 +2021,14 @@ static void launch_hmac_var_mode(int mode, unsigned grid, hipStream_t s,
 hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
     uint64_t stride, uint32_t fixed_len, uint64_t n, uint8_t *out,
-    uint32_t *ws, hipStream_t s, int mode, const BurstRx *burst_rx)
+    uint32_t *ws, hipStream_t s, int mode, const BurstArgs *burst_args)
 {
 	if (mode != HMAC_DIGESTS && offsets == nullptr)
 		return hipErrorInvalidValue;	/* datagram modes: var layout */
 	if ((mode == HMAC_BURST_RX || mode == HMAC_BURST_TX) !=
-	    (burst_rx != nullptr))
+	    (burst_args != nullptr))
 		return hipErrorInvalidValue;
-	const BurstRx rx = burst_rx ? *burst_rx : BurstRx{};
+	const BurstArgs rx = burst_args ? *burst_args : BurstArgs{};
 	if (n == 0)
 		return hipSuccess;
 	const int halg = alg - 3;	/* HMAC row -> SHA row */

@@ -52,27 +52,27 @@ hipError_t net2_bin_order(int alg, const uint32_t *lens, uint64_t n,
  * lens are whole wire datagrams; each lane decodes the 8-byte header, sets
  * status (NET2_PDECODE_* | 0x80 when the verdict decides), seq and flags,
  * and verifies "hash field || payload" after the header into out[i] as in
- * mode 2.  Requires burst_rx.
+ * mode 2.  Requires burst_args.
  */
 #define NET2_HMAC_MODE_BURST_RX 3
 /*
  * 4: the TX burst (net2_packet_encode_burst with a hash key, out = base):
  * seq / flags are the caller's per-datagram inputs; each lane checks the
  * flags and the room, writes the 8-byte header, signs the payload into the
- * hash field after it and sets status.  Requires burst_rx.
+ * hash field after it and sets status.  Requires burst_args.
  */
 #define NET2_HMAC_MODE_BURST_TX 4
-struct BurstRx {
+struct BurstArgs {
 	uint32_t *seq;		/* RX: out; TX: in */
 	uint32_t *flags;	/* RX: out; TX: in */
-	uint8_t *status;
-	int enc_set;
+	uint8_t *status;	/* RX: code | 0x80 (verdict pending); TX: final code */
+	int enc_set;		/* a cipher key is set */
 };
 hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
     uint64_t stride, uint32_t fixed_len, uint64_t n, uint8_t *out,
     uint32_t *ws, hipStream_t s, int mode = NET2_HMAC_MODE_DIGESTS,
-    const BurstRx *burst_rx = nullptr);
+    const BurstArgs *burst_args = nullptr);
 
 /*
  * Coalesced small jobs (sha2_coalesce.cpp): many independent requests from

@@ -1111,7 +1111,7 @@ NET2_EXPORT int net2_packet_decode_burst(int hash_alg, const void *hash_key,
 	if (hash_set) {
 		/* header decode, flag checks and HMAC verify in one kernel over
 		 * the wire datagrams (binned by datagram length) */
-		const BurstRx rx = { seq, flags, w.status, enc_alg != 0 };
+		const BurstArgs rx = { seq, flags, w.status, enc_alg != 0 };
 		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)hash_key,
 		    hash_keylen, (const uint8_t *)d_base, d_offsets, d_lens, 0,
 		    0, n, w.verdict, w.bin, s, NET2_HMAC_MODE_BURST_RX, &rx));
@@ -1145,7 +1145,7 @@ NET2_EXPORT int net2_packet_encode_burst(int hash_alg, const void *hash_key,
 		/* flag and room checks, header write and HMAC sign in one
 		 * kernel over the wire datagrams; the TX code is final (no
 		 * verdict to fold in), so the kernel writes it to d_result */
-		const BurstRx tx = { const_cast<uint32_t *>(d_seq),
+		const BurstArgs tx = { const_cast<uint32_t *>(d_seq),
 		    const_cast<uint32_t *>(d_flags), d_result, enc_alg != 0 };
 		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)hash_key,
 		    hash_keylen, (const uint8_t *)d_base, d_offsets, d_lens, 0,
