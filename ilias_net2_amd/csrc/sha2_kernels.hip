@@ -1430,6 +1430,18 @@ __device__ __forceinline__ void ph_iv_one(uint32_t s, uint32_t f,
 		for (int j = 0; j < 8; j++)
 			d[8 * r + j] = st[j];
 	}
+	/* 16-byte stores when the IV is whole 16-byte pieces at an aligned
+	 * address (AES's 16-byte IV in an n x 16 array), bytes otherwise */
+	if ((ivlen & 15) == 0 && (reinterpret_cast<uintptr_t>(o) & 15) == 0) {
+		uint4 *q = reinterpret_cast<uint4 *>(o);
+#pragma unroll
+		for (int k = 0; k < 4; k++)
+			if (16u * k < ivlen)
+				q[k] = make_uint4(bswap32(d[4 * k]),
+				    bswap32(d[4 * k + 1]), bswap32(d[4 * k + 2]),
+				    bswap32(d[4 * k + 3]));
+		return;
+	}
 	for (uint32_t b = 0; b < ivlen; b++)
 		o[b] = (uint8_t)(d[b >> 2] >> (24 - 8 * (b & 3)));
 }
