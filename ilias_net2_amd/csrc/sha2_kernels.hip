@@ -975,8 +975,24 @@ __device__ __forceinline__ uint32_t load_be32_bytes(const uint8_t *p)
 #define NET2_VERIFY_WORDS 1
 #endif
 
+/*
+ * Occupancy of the SHA-512 HMAC kernels: NET2_HMAC512_W5 has bit MODE set
+ * for the modes compiled for 5 waves per SIMD (96 VGPRs, some scratch
+ * spills) instead of the 4 their 114-118 VGPRs give.  Digests: HMAC-SHA512
+ * 1 KiB +4.2 %, the MTU mix +2.2 %; the RX burst mode -14.6 % (it spills
+ * three times as much) (profiles/round2/hmac512_waves_ab.txt).
+ */
+#ifndef NET2_HMAC512_W5
+#define NET2_HMAC512_W5 0x1
+#endif
+template <class H, int MODE>
+struct HmacWaves {
+	static constexpr int value = sizeof(typename H::word) == 8 &&
+	    ((NET2_HMAC512_W5 >> MODE) & 1) ? 5 : 1;
+};
 template <class H, bool PADCONST, int MODE = HMAC_DIGESTS>
-__global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ base,
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(HmacWaves<H, MODE>::value))) void hmac_kernel(const uint8_t *__restrict__ base,
     const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
     const uint32_t *__restrict__ perm, uint64_t stride, uint32_t fixed_len,
     uint64_t n, uint8_t *__restrict__ out, uint32_t dlen, int is384,
