@@ -585,8 +585,18 @@ __device__ __forceinline__ void fixed_lane(uint64_t i,
 		store_digest<H::DLEN>(out + i * H::DLEN, o);
 }
 
+/* waves per SIMD asked of the fixed SHA-512 kernel (A/B; 1 = no request) */
+#ifndef NET2_FIXED512_WAVES
+#define NET2_FIXED512_WAVES 1
+#endif
+template <class H>
+struct FixedWaves {
+	static constexpr int value = sizeof(typename H::word) == 8 ?
+	    NET2_FIXED512_WAVES : 1;
+};
 template <class H, int AMODE, bool PADCONST>
-__global__ __launch_bounds__(256) void fixed_kernel(const uint8_t *__restrict__ base,
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(FixedWaves<H>::value))) void fixed_kernel(const uint8_t *__restrict__ base,
     uint64_t stride, uint32_t len, uint64_t n, uint8_t *__restrict__ out,
     uint32_t dlen, int is384, PadKW<typename H::word> pad)
 {
@@ -759,16 +769,22 @@ __device__ __forceinline__ void var_digest(const uint8_t *p, uint32_t len,
  * workgroup) of one whole-block length, e.g. a bin of a batch of fixed
  * sizes, takes its pad schedule from g_padtab256 (g_padtab512).
  */
-#ifndef NET2_VAR_WAVES
-#define NET2_VAR_WAVES 0
+/* waves per SIMD asked of the variable-length kernel, per word size
+ * (A/B; 1 = no request: the VGPR count decides) */
+#ifndef NET2_VAR256_WAVES
+#define NET2_VAR256_WAVES 1
 #endif
-#if NET2_VAR_WAVES > 0
-#define NET2_VAR_ATTR __attribute__((amdgpu_waves_per_eu(NET2_VAR_WAVES)))
-#else
-#define NET2_VAR_ATTR
+#ifndef NET2_VAR512_WAVES
+#define NET2_VAR512_WAVES 1
 #endif
 template <class H>
-__global__ __launch_bounds__(256) NET2_VAR_ATTR void var_kernel(const uint8_t *__restrict__ base,
+struct VarWaves {
+	static constexpr int value = sizeof(typename H::word) == 8 ?
+	    NET2_VAR512_WAVES : NET2_VAR256_WAVES;
+};
+template <class H>
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(VarWaves<H>::value))) void var_kernel(const uint8_t *__restrict__ base,
     const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
     const uint32_t *__restrict__ perm, uint64_t n, uint8_t *__restrict__ out,
     uint32_t dlen, int is384)
