@@ -125,13 +125,18 @@ typedef Sha256T<NET2_VAR_ASM != 0, NET2_VAR_U2 != 0, NET2_VAR_PAIR != 0,
     NET2_VAR256_DRAIN != 0> Sha256V;	/* var */
 typedef Sha256T<NET2_HMAC_ASM != 0, NET2_HMAC_U2 != 0, NET2_HMAC_PAIR != 0> Sha256H;	/* HMAC */
 
+#ifndef NET2_FIXED512_PF
+#define NET2_FIXED512_PF 0
+#endif
 /* drain priority in the fixed SHA-512 kernel (prio_remaining below) */
 #ifndef NET2_SHA512_DRAIN
 #define NET2_SHA512_DRAIN 1
 #endif
 struct Sha512 {
 	static constexpr bool ASM = false;
-	static constexpr bool U2 = false;	/* no prefetch: nothing to ping-pong */
+	/* no prefetch: nothing to ping-pong (NET2_FIXED512_PF=1: the two-block
+	 * ping-pong prefetch, A/B only) */
+	static constexpr bool U2 = NET2_FIXED512_PF != 0;
 	static constexpr bool PAIR = false;	/* a 128-byte block is a whole line */
 	/* drain priority (prio_remaining): the fixed kernel only */
 	static constexpr bool DRAIN = NET2_SHA512_DRAIN != 0;
@@ -141,7 +146,7 @@ struct Sha512 {
 	static constexpr int LENBYTES = 16;
 	static constexpr int DLEN = 64;		/* 48 for SHA-384 */
 	/* a 128-byte prefetch would cost 32 VGPRs and a wave per SIMD */
-	static constexpr bool PREFETCH = false;
+	static constexpr bool PREFETCH = NET2_FIXED512_PF != 0;
 	typedef uint64_t State[8];
 
 	__device__ __forceinline__ static void init(State &st, int is384)
