@@ -1006,10 +1006,14 @@ __device__ __forceinline__ uint32_t load_be32_bytes(const uint8_t *p)
 #ifndef NET2_HMAC512_W5
 #define NET2_HMAC512_W5 0x1
 #endif
+/* the same for the SHA-256 HMAC kernels (A/B; 0 = none) */
+#ifndef NET2_HMAC256_W5
+#define NET2_HMAC256_W5 0x0
+#endif
 template <class H, int MODE>
 struct HmacWaves {
-	static constexpr int value = sizeof(typename H::word) == 8 &&
-	    ((NET2_HMAC512_W5 >> MODE) & 1) ? 5 : 1;
+	static constexpr int value = (sizeof(typename H::word) == 8 ?
+	    NET2_HMAC512_W5 : NET2_HMAC256_W5) >> MODE & 1 ? 5 : 1;
 };
 template <class H, bool PADCONST, int MODE = HMAC_DIGESTS>
 __global__ __launch_bounds__(256)
