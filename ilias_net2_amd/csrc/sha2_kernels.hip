@@ -391,6 +391,15 @@ __device__ __forceinline__ void prio_remaining(uint32_t rem_blocks)
  * whose K[t] + W[t] schedule the host precomputed (kw).
  */
 /*
+ * NET2_PAIR_LATE=1 (A/B): the pair loop requests the next pair after the
+ * first compression of the current one instead of before it, so a grid's
+ * first wave generation asks HBM for one line per lane, not two, before it
+ * can start.
+ */
+#ifndef NET2_PAIR_LATE
+#define NET2_PAIR_LATE 0
+#endif
+/*
  * SHA*Update over the len / BLOCK full blocks at p (src/sha2.c:477-485:
  * whole blocks are transformed straight from caller memory).  With
  * PREFETCH, block k+1 is loaded while block k is compressed.
@@ -424,11 +433,17 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 		for (; q + 2 <= npairs; q += 2) {
 			prio_remaining<H::DRAIN>(nfull - 2 * q);
 			const uint8_t *bp = p + (size_t)q * 2 * H::BLOCK;
-			issue_block<NW32, AMODE>(bp + 2 * H::BLOCK, b0);
-			issue_block<NW32, AMODE>(bp + 3 * H::BLOCK, b1);
+			if (!NET2_PAIR_LATE) {
+				issue_block<NW32, AMODE>(bp + 2 * H::BLOCK, b0);
+				issue_block<NW32, AMODE>(bp + 3 * H::BLOCK, b1);
+			}
 			uint32_t w[NW32];
 			finish_block<NW32, AMODE>(bp, a0, w);
 			H::compress(st, w);
+			if (NET2_PAIR_LATE) {
+				issue_block<NW32, AMODE>(bp + 2 * H::BLOCK, b0);
+				issue_block<NW32, AMODE>(bp + 3 * H::BLOCK, b1);
+			}
 			finish_block<NW32, AMODE>(bp + H::BLOCK, a1, w);
 			H::compress(st, w);
 			/* past the last pair: re-read pair q + 1 (in bounds, L2-hot,
