@@ -115,8 +115,9 @@ typedef Sha256T<NET2_ASM256 != 0, NET2_ABSORB_U2 != 0, NET2_FIXED_PAIR != 0> Sha
 #ifndef NET2_VAR_PAIR
 #define NET2_VAR_PAIR 1
 #endif
-/* drain priority (prio_remaining) in the variable-length kernel: A/B only,
- * off -- C3 +1.4 %, the byte-aligned mix -0.6 %
+/* drain priority (prio_remaining) in the variable-length kernel (A/B only,
+ * off): +1.1 to +1.4 % on C3 when run second in each alternation, -0.6 %
+ * when run first -- within the position effect of the A/B itself
  * (profiles/round2/var_drain_ab.txt) */
 #ifndef NET2_VAR256_DRAIN
 #define NET2_VAR256_DRAIN 0
@@ -341,7 +342,8 @@ __device__ __forceinline__ void materialize(const typename H::State &st)
 }
 
 /*
- * Issue priority while a grid drains (H::DRAIN: the fixed SHA-512 kernel).
+ * Issue priority while a grid drains (H::DRAIN: the fixed SHA-512 kernel;
+ * not on the byte-aligned load path).
  * The SIMD's VALU arbiter serves the oldest wave first, so when the grid's
  * last generation of waves is dispatched, the youngest waves -- those with
  * the most blocks left -- progress last and finish alone, at one wave's
@@ -431,7 +433,7 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 		}
 		uint32_t q = 0;
 		for (; q + 2 <= npairs; q += 2) {
-			prio_remaining<H::DRAIN>(nfull - 2 * q);
+			prio_remaining<H::DRAIN && AMODE != AMODE_A1>(nfull - 2 * q);
 			const uint8_t *bp = p + (size_t)q * 2 * H::BLOCK;
 			if (!NET2_PAIR_LATE) {
 				issue_block<NW32, AMODE>(bp + 2 * H::BLOCK, b0);
@@ -483,7 +485,7 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 			issue_block<NW32, AMODE>(p, ra);
 		uint32_t k = 0;
 		for (; k + 2 <= nfull; k += 2) {
-			prio_remaining<H::DRAIN>(nfull - k);
+			prio_remaining<H::DRAIN && AMODE != AMODE_A1>(nfull - k);
 			const uint8_t *bp = p + (size_t)k * H::BLOCK;
 			issue_block<NW32, AMODE>(bp + H::BLOCK, rb);
 			uint32_t w[NW32];
@@ -511,7 +513,7 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 		if (nfull > 0)
 			issue_block<NW32, AMODE>(p, cur);
 		for (uint32_t k = 0; k < nfull; k++) {
-			prio_remaining<H::DRAIN>(nfull - k);
+			prio_remaining<H::DRAIN && AMODE != AMODE_A1>(nfull - k);
 			const uint8_t *bp = p + (size_t)k * H::BLOCK;
 			Raw<NW32> nxt;
 			if (k + 1 < nfull)
@@ -523,7 +525,7 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 		}
 	} else {
 		for (uint32_t k = 0; k < nfull; k++) {
-			prio_remaining<H::DRAIN>(nfull - k);
+			prio_remaining<H::DRAIN && AMODE != AMODE_A1>(nfull - k);
 			const uint8_t *bp = p + (size_t)k * H::BLOCK;
 			Raw<NW32> cur;
 			issue_block<NW32, AMODE>(bp, cur);
