@@ -98,9 +98,13 @@ struct Sha256T {
 #endif
 /* prefetch in the byte-aligned (A1) path of the variable-length and HMAC
  * kernels: every path of a kernel shares its VGPR allocation, and the A1
- * path's double buffer (17 words each) sets it */
+ * path's double buffer (17 words each) sets it.  Variable-length kernel:
+ * off since the end of round 2 -- 96 VGPRs (5 waves per SIMD) instead of
+ * 105, byte-aligned mix +0.7 %, C3 +0.3 % with the A/B order flipped
+ * every alternation (profiles/round2/var_a1_prefetch_ab.txt; the earlier
+ * -1.6 % on C3 was measured with the variant always second) */
 #ifndef NET2_VAR_A1_PREFETCH
-#define NET2_VAR_A1_PREFETCH 1
+#define NET2_VAR_A1_PREFETCH 0
 #endif
 #ifndef NET2_HMAC_A1_PREFETCH
 #define NET2_HMAC_A1_PREFETCH 1
