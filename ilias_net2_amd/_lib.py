@@ -32,6 +32,16 @@ class IOVec(ctypes.Structure):
     _fields_ = [("iov_base", ctypes.c_void_p), ("iov_len", ctypes.c_size_t)]
 
 
+class BurstRxKeys(ctypes.Structure):
+    """struct net2_burst_rx_keys (include/net2/packet.h)."""
+    _fields_ = [("hash_alg", ctypes.c_int), ("hash_key", ctypes.c_void_p),
+                ("hash_keylen", ctypes.c_size_t), ("enc_alg", ctypes.c_int),
+                ("alt_hash_key", ctypes.c_void_p),
+                ("alt_hash_keylen", ctypes.c_size_t),
+                ("alt_no_cutoff", ctypes.c_int), ("alt_cutoff", ctypes.c_uint32),
+                ("rx_start", ctypes.c_uint32)]
+
+
 _c_u64p = ctypes.POINTER(ctypes.c_uint64)
 _c_u32p = ctypes.POINTER(ctypes.c_uint32)
 
@@ -88,6 +98,11 @@ SIGNATURES = {
         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
         ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "net2_packet_decode_burst_ck": (ctypes.c_int, [
+        ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+        ctypes.c_void_p]),
     "net2_packet_encode_burst": (ctypes.c_int, [
         ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

@@ -40,6 +40,10 @@ static const char *const sign_names[] = { "ecdsa" };
 NET2_EXPORT const int net2_signmax =
     (int)(sizeof(sign_names) / sizeof(sign_names[0]));
 
+/* The ECDSA row of the registry, by name (src/sign.c:653; test/sign.c:66,69
+ * pass it to net2_signctx_{priv,pub}new). */
+NET2_EXPORT const int net2_sign_ecdsa = 0;
+
 NET2_EXPORT const char *
 net2_sign_getname(int alg)
 {

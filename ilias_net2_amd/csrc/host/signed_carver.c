@@ -173,7 +173,8 @@ ecdsa_run(void *arg)
 			const size_t r = sign_req_of(pl, j);
 			struct net2_sc_sign_req *q = &pl->sreq[r];
 			const size_t k = j - pl->sjob[r];
-			if (q->rc != 0)
+			/* a sibling signature may have failed already */
+			if (__atomic_load_n(&q->rc, __ATOMIC_RELAXED) != 0)
 				continue;
 			int rc = sign_digest(&q->out[k], pl->sdig + 64 * r,
 			    (size_t)net2_hash_gethashlen(q->hash_alg),
@@ -295,12 +296,10 @@ tick(struct net2_sc_sign_req *sreq, size_t ns,
 		p[np++] = (struct payload_ref){ q->payload, q->iovcnt, valg[i],
 		    vdig + 64 * i, &q->result };
 	}
-	/* one GPU batch per hash algorithm */
-	for (int alg = NET2_HASH_SHA256; alg <= NET2_HASH_SHA512; alg++) {
-		int r = hash_group(p, np, alg);
-		if (r != 0 && rc == 0)
-			rc = r;
-	}
+	/* one GPU batch per hash algorithm; a group's failure is in the rc /
+	 * result of each of its requests (hash_group), so the others go on */
+	for (int alg = NET2_HASH_SHA256; alg <= NET2_HASH_SHA512; alg++)
+		(void)hash_group(p, np, alg);
 	for (size_t i = 0; i < nv; i++)
 		if (vreq[i].result != 0) {
 			vreq[i].result = EIO;	/* hash failure: :333-336 */
@@ -325,13 +324,23 @@ tick(struct net2_sc_sign_req *sreq, size_t ns,
 		    sreq[i].rc != EINVAL)
 			for (uint32_t k = 0; k < sreq[i].num_signatures; k++)
 				net2_signature_deinit(&sreq[i].out[k]);
-	if (rc == 0 && ns > 0) {
-		/* the batch failed as a whole only if every carver failed */
-		int all = 1;
-		for (size_t i = 0; i < ns && all; i++)
+	/* the tick failed as a whole only if every request did (a validation
+	 * that ran and found the signature invalid, EINVAL, is an outcome, not
+	 * a failure); then it returns the first request's error, which every
+	 * request carries too.  Otherwise 0, and the per-request rc / result
+	 * values are the outcome. */
+	if (ns + nv > 0) {
+		int all = 1, first = 0;
+		for (size_t i = 0; i < ns && all; i++) {
 			all = sreq[i].rc != 0;
-		if (all && nv == 0)
-			rc = sreq[0].rc;
+			first = first ? first : sreq[i].rc;
+		}
+		for (size_t i = 0; i < nv && all; i++) {
+			all = vreq[i].result == EIO;
+			first = first ? first : vreq[i].result;
+		}
+		if (all)
+			rc = first;
 	}
 out:
 	free(p);

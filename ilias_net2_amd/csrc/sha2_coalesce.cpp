@@ -52,6 +52,10 @@ typedef std::chrono::steady_clock clk;
 
 constexpr int kMaxSlots = 16;
 constexpr size_t kInitialStage = 1u << 20;	/* grows on demand */
+/* staging grown past this for one large request is released once its
+ * batch completes, so a few big hashiov / Update calls do not keep
+ * gigabytes page-locked for the life of the process */
+constexpr size_t kRetainStage = 16u << 20;
 constexpr size_t kMaxJobs = 1u << 16;		/* per batch */
 /*
  * Up to this many jobs a batch runs one wave per job (job_wave_kernel, the
@@ -63,6 +67,10 @@ constexpr size_t kMaxJobs = 1u << 16;		/* per batch */
  * (SHA-256: 433 k vs 349 k calls/s).
  */
 constexpr size_t kWaveJobsMax = 16;
+/* ... and any job this long takes the wave form whatever the batch size: in
+ * the lane form one lane runs every compression of its job in turn, a
+ * 4 GiB message for minutes (64 KiB of SHA-256, 128 KiB of SHA-512) */
+constexpr uint32_t kWaveBlocks = 1024;
 
 int env_int(const char *name, int dflt, int lo, int hi)
 {
@@ -411,6 +419,9 @@ int Coalescer::submit(int ordinal, const Request &r, int *hip_err)
 		futex_wake(w);		/* jp may be gone now; the address is inert */
 	}
 
+	/* the slot is still ours (not on free_): shrink outside the lock */
+	if (s.cap > kRetainStage)
+		s.free_stage();
 	lk.lock();
 	s.jobs.clear();
 	inflight_--;
@@ -469,7 +480,7 @@ int Coalescer::launch_and_wait(Slot &s, int ordinal, int *hip_err)
 	std::vector<Job *> &jobs = s.jobs;
 	const size_t n = jobs.size();
 	size_t hdr_off, n256;
-	uint32_t waves, target;
+	uint32_t waves, target, maxblk = 0;
 	int wave;
 	const uint8_t *stage;
 	uint8_t *d_out;
@@ -513,6 +524,7 @@ int Coalescer::launch_and_wait(Slot &s, int ordinal, int *hip_err)
 		memcpy(s.h_stage + hdr_off + k * sizeof(Net2Job), &jobs[k]->desc,
 		    sizeof(Net2Job));
 		n256 += jobs[k]->alg == 1;
+		maxblk = std::max(maxblk, jobs[k]->desc.nblk);
 	}
 	if (!zerocopy_)
 		CO_TRY(hipMemcpyAsync(s.d_stage, s.h_stage,
@@ -521,7 +533,8 @@ int Coalescer::launch_and_wait(Slot &s, int ordinal, int *hip_err)
 	stage = s.d_stage;
 	/* few jobs: a wave each (lower latency, the GPU is idle anyway);
 	 * many: a lane each */
-	wave = jobmode_ == 1 || (jobmode_ == 0 && n <= kWaveJobsMax);
+	wave = jobmode_ == 1 || (jobmode_ == 0 && (n <= kWaveJobsMax ||
+	    maxblk >= kWaveBlocks));
 	waves = wave ? (uint32_t)n :
 	    (uint32_t)((n256 + 63) / 64 + (n - n256 + 63) / 64);
 	target = s.done_base + waves;

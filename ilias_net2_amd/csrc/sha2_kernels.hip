@@ -45,6 +45,8 @@ struct Sha256T {
 	static constexpr bool U2 = U2_;
 	static constexpr bool PAIR = PAIR_;
 	static constexpr bool DRAIN = DRAIN_;	/* prio_remaining */
+	static constexpr bool GLDS = false;	/* absorb: LDS-DMA staging */
+	static constexpr bool FLAT = false;	/* digest_flat */
 	typedef uint32_t word;
 	static constexpr int BLOCK = 64;	/* bytes per block */
 	static constexpr int NW32 = 16;		/* 32-bit words per block */
@@ -145,6 +147,8 @@ struct Sha512 {
 	static constexpr bool PAIR = false;	/* a 128-byte block is a whole line */
 	/* drain priority (prio_remaining): the fixed kernel only */
 	static constexpr bool DRAIN = NET2_SHA512_DRAIN != 0;
+	static constexpr bool GLDS = false;
+	static constexpr bool FLAT = false;
 	typedef uint64_t word;
 	static constexpr int BLOCK = 128;
 	static constexpr int NW32 = 32;
@@ -180,6 +184,21 @@ struct Sha512 {
 	}
 };
 
+/*
+ * NET2_GLDS512 (bit per kernel family: 1 variable-length SHA-512, 2 the
+ * variable-length HMAC-SHA512 kernels incl. bursts, 4 the fixed-layout
+ * HMAC-SHA512 kernel): the next 128-byte block is fetched with LDS-DMA
+ * (global_load_lds) into a per-wave LDS slab while the current one is
+ * compressed -- a prefetch that costs no VGPRs (absorb below).
+ */
+#ifndef NET2_GLDS512
+#define NET2_GLDS512 0x4
+#endif
+/* NET2_FLAT512: the same families with every compression at one call site
+ * (digest_flat) */
+#ifndef NET2_FLAT512
+#define NET2_FLAT512 0
+#endif
 /* SHA-512 for the variable-length kernel; NET2_VAR512_PF=1 (A/B only)
  * gives it the two-block ping-pong prefetch the SHA-256 kernels have. */
 #ifndef NET2_VAR512_PF
@@ -187,8 +206,10 @@ struct Sha512 {
 #endif
 struct Sha512V : Sha512 {
 	static constexpr bool DRAIN = false;
-	static constexpr bool U2 = NET2_VAR512_PF != 0;
-	static constexpr bool PREFETCH = NET2_VAR512_PF != 0;
+	static constexpr bool GLDS = (NET2_GLDS512 & 1) != 0;
+	static constexpr bool FLAT = (NET2_FLAT512 & 1) != 0;
+	static constexpr bool U2 = NET2_VAR512_PF != 0 && !GLDS;
+	static constexpr bool PREFETCH = NET2_VAR512_PF != 0 && !GLDS;
 };
 /* ... for the lane-per-job kernel of the coalescer (NET2_JOB512_PF, on),
  * whose blocks come over PCIe from zero-copy staging: the next block's
@@ -209,8 +230,15 @@ struct Sha512J : Sha512 {
 #endif
 struct Sha512H : Sha512 {
 	static constexpr bool DRAIN = false;
-	static constexpr bool U2 = NET2_HMAC512_PF != 0;
-	static constexpr bool PREFETCH = NET2_HMAC512_PF != 0;
+	static constexpr bool GLDS = (NET2_GLDS512 & 2) != 0;
+	static constexpr bool FLAT = (NET2_FLAT512 & 2) != 0;
+	static constexpr bool U2 = NET2_HMAC512_PF != 0 && !GLDS;
+	static constexpr bool PREFETCH = NET2_HMAC512_PF != 0 && !GLDS;
+};
+/* ... and for the fixed-layout HMAC-SHA512 kernel (drain priority kept) */
+struct Sha512HF : Sha512 {
+	static constexpr bool GLDS = (NET2_GLDS512 & 4) != 0;
+	static constexpr bool FLAT = (NET2_FLAT512 & 4) != 0;
 };
 
 /* ---- message loading ------------------------------------------------- */
@@ -227,6 +255,13 @@ struct Sha512H : Sha512 {
 enum { AMODE_A16 = 0, AMODE_A1 = 1, AMODE_A4 = 2 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+/*
+ * Dword loads from an address rebuilt from an integer (the aligned-down
+ * start of a byte-aligned packet) go through a global pointer: a plain
+ * pointer would be a flat load, which may alias LDS, and in a kernel with
+ * LDS-DMA in flight every flat load waits for all outstanding loads first.
+ */
+typedef __attribute__((address_space(1))) const uint32_t gconst_u32;
 
 template <int NW32>
 struct Raw {
@@ -253,7 +288,7 @@ __device__ __forceinline__ void issue_block(const uint8_t *p, Raw<NW32> &r)
 			r.d[i] = q[i];
 	} else {
 		uintptr_t a = reinterpret_cast<uintptr_t>(p);
-		const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+		const gconst_u32 *q = (const gconst_u32 *)(a & ~(uintptr_t)3);
 #pragma unroll
 		for (int i = 0; i < NW32; i++)
 			r.d[i] = q[i];
@@ -280,6 +315,66 @@ __device__ __forceinline__ void finish_block(const uint8_t *p,
 }
 
 /*
+ * LDS-DMA staging (H::GLDS).  A global_load_lds instruction writes the
+ * wave's 64 lane chunks to LDS lane-linearly (wave-uniform base + lane x
+ * size), with no VGPR destination.  Chunk j (16 bytes) of every lane's
+ * block goes to its own 1 KiB row of the wave's slab, so lane l reads its
+ * block back from its own column with ds_read_b128 (consecutive lanes,
+ * consecutive banks).  All address modes fetch 16-byte chunks: A16 and A4
+ * from the block start (a global dwordx4 needs only dword alignment), A1
+ * from the naturally aligned dword below it, plus the one dword past the
+ * 32nd into a 256-byte row of its own when the start is misaligned -- the
+ * bytes issue_block reads, never one outside the packet.  (Dword-wide
+ * fetches, 32 per block, measured 35-42 % slower on the variable-length
+ * SHA-512 kernels: every instruction touches the wave's 64 lines.)
+ * One 8,448-byte slab per wave of a 256-thread workgroup.
+ */
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+#define NET2_GLDS_WORDS (33 * 64)
+__shared__ uint32_t glds_slab[4 * NET2_GLDS_WORDS];
+
+__device__ __forceinline__ uint32_t *glds_wave_slab()
+{
+	const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	return glds_slab + wv * NET2_GLDS_WORDS;
+}
+
+template <int NW32, int AMODE>
+__device__ __forceinline__ void glds_issue(const uint8_t *p, uint32_t *slab)
+{
+	const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+	const uint8_t *q = AMODE != AMODE_A1 ? p :
+	    reinterpret_cast<const uint8_t *>(a & ~(uintptr_t)3);
+#pragma unroll
+	for (int j = 0; j < NW32 / 4; j++)
+		__builtin_amdgcn_global_load_lds((glb_void *)(q + 16 * j),
+		    (lds_void *)(slab + 256 * j), 16, 0, 0);
+	if (AMODE == AMODE_A1 && (a & 3))
+		__builtin_amdgcn_global_load_lds((glb_void *)(q + 4 * NW32),
+		    (lds_void *)(slab + 64 * NW32), 4, 0, 0);
+}
+
+/* The lane's staged block back from the slab, as issue_block leaves it. */
+template <int NW32, int AMODE>
+__device__ __forceinline__ void glds_read(const uint32_t *slab, Raw<NW32> &r)
+{
+	const uint32_t lane = threadIdx.x & 63;
+	const u32x4 *s = reinterpret_cast<const u32x4 *>(slab) + lane;
+#pragma unroll
+	for (int j = 0; j < NW32 / 4; j++) {
+		const u32x4 v = s[64 * j];
+		r.d[4 * j] = v.x;
+		r.d[4 * j + 1] = v.y;
+		r.d[4 * j + 2] = v.z;
+		r.d[4 * j + 3] = v.w;
+	}
+	/* the A1 dword past the 32nd; unused when the start is aligned
+	 * (alignbyte by 0) */
+	r.d[NW32] = AMODE == AMODE_A1 ? slab[64 * NW32 + lane] : 0u;
+}
+
+/*
  * The last data bytes q[0 .. rem) (rem < BLOCK) followed by the 0x80
  * terminator and zero fill, as big-endian words (the buffer SHA256Pad /
  * SHA512Pad build, src/sha2.c:495-526 / :784-812).  Only dwords that hold
@@ -291,7 +386,7 @@ __device__ __forceinline__ void tail_block(const uint8_t *q, uint32_t rem,
 {
 	uintptr_t a = reinterpret_cast<uintptr_t>(q);
 	uint32_t sh = (uint32_t)a & 3;
-	const uint32_t *al = reinterpret_cast<const uint32_t *>(a - sh);
+	const gconst_u32 *al = (const gconst_u32 *)(a - sh);
 	uint32_t d[NW32 + 1];
 #pragma unroll
 	for (int j = 0; j <= NW32; j++)
@@ -417,7 +512,31 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 	constexpr int NW32 = H::NW32;
 	const uint32_t nfull = len / H::BLOCK;
 
-	if (PREFETCH && H::PAIR) {
+	if constexpr (H::GLDS) {
+		/*
+		 * Block k+1 is requested into the wave's LDS slab (no VGPRs)
+		 * once block k has been read out of it, so its memory latency
+		 * runs under block k's compression.  The waits are explicit:
+		 * the slab is complete after vmcnt(0), and free again once the
+		 * lane's reads have returned (lgkmcnt(0)).
+		 */
+		uint32_t *slab = glds_wave_slab();
+		if (nfull > 0)
+			glds_issue<NW32, AMODE>(p, slab);
+		for (uint32_t k = 0; k < nfull; k++) {
+			prio_remaining<H::DRAIN && AMODE != AMODE_A1>(nfull - k);
+			const uint8_t *bp = p + (size_t)k * H::BLOCK;
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			Raw<NW32> r;
+			glds_read<NW32, AMODE>(slab, r);
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+			if (k + 1 < nfull)
+				glds_issue<NW32, AMODE>(bp + H::BLOCK, slab);
+			uint32_t w[NW32];
+			finish_block<NW32, AMODE>(bp, r, w);
+			H::compress(st, w);
+		}
+	} else if (PREFETCH && H::PAIR) {
 		/*
 		 * Pairs of blocks (one 128-byte line of an aligned packet)
 		 * requested together, one pair ahead: two pair buffers swap
@@ -772,6 +891,137 @@ __device__ __forceinline__ bool block_pad512(bool live, uint64_t bytes)
 	return true;
 }
 
+/* The state as big-endian digest words (SHA*Final's byte order). */
+template <class H>
+__device__ __forceinline__ int digest_words(const typename H::State &st,
+    int is384, uint32_t (&w)[H::NW32])
+{
+	if (sizeof(typename H::word) == 4) {
+#pragma unroll
+		for (int i = 0; i < 8; i++)
+			w[i] = (uint32_t)st[i];
+		return 8;
+	}
+#pragma unroll
+	for (int i = 0; i < 8; i++) {
+		w[2 * i] = hi32((uint64_t)st[i]);
+		w[2 * i + 1] = lo32((uint64_t)st[i]);
+	}
+	return is384 ? 12 : 16;
+}
+
+/* Midstate `which` (0 inner, 1 outer) from LDS into a state. */
+template <class H>
+__device__ __forceinline__ void load_mid(const uint32_t (*mid)[16], int which,
+    typename H::State &st)
+{
+	/* opaque zero: keeps the reads where they are written (not hoisted
+	 * and shared across the address-mode branches) */
+	uint32_t z;
+	asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+	mid += z;
+#pragma unroll
+	for (int i = 0; i < 8; i++) {
+		if (sizeof(typename H::word) == 4)
+			st[i] = mid[which][i];
+		else
+			st[i] = mk64(mid[which][2 * i + 1], mid[which][2 * i]);
+	}
+}
+
+/*
+ * Every compression of one lane's message at one call site (H::FLAT): the
+ * data blocks, the tail block (data remainder, 0x80, zero fill, bit count),
+ * the zero block SHA*Pad adds when the count does not fit
+ * (src/sha2.c:505-519 / :794-808) and, for HMAC, the outer block, each
+ * iteration of one loop picking its block.  Spelled out as in
+ * absorb + finish + the HMAC outer step, a SHA-512 lane's code holds four
+ * or five unrolled compressions of ~28 KB each (five or six with the pad
+ * table's); a workgroup's waves run them all at once, well past the
+ * instruction cache.  Here the kernel holds one (plus the pad-table form
+ * when used).  A wave whose lanes share a length runs the loop in
+ * lockstep; binned batches make that the common case.
+ *   padtab: the pad block is the whole-block-length constant one, its
+ *           K + W schedule at kw (SHA-256) / in k512_lds (SHA-512);
+ *   HM:     HMAC -- start from the inner midstate, end with the outer block
+ *           from the outer one (mid, as hmac_kernel stages them).
+ */
+template <class H, int AMODE, bool HM>
+__device__ __forceinline__ void digest_flat(const uint8_t *p, uint32_t len,
+    uint64_t bits, int is384, const typename H::word *kw, bool padtab,
+    const uint32_t (*mid)[16], typename H::State &st)
+{
+	constexpr int NW32 = H::NW32;
+	const uint32_t nfull = len / H::BLOCK;
+	const uint32_t rem = len % H::BLOCK;
+	const bool extra = !padtab && rem >= (uint32_t)(H::BLOCK - H::LENBYTES);
+	const uint32_t nblk = nfull + 1 + (extra ? 1 : 0) + (HM ? 1 : 0);
+	if (HM)
+		load_mid<H>(mid, 0, st);
+	else
+		H::init(st, is384);
+	uint32_t *slab = nullptr;
+	if constexpr (H::GLDS) {
+		slab = glds_wave_slab();
+		if (nfull > 0)
+			glds_issue<NW32, AMODE>(p, slab);
+	}
+	for (uint32_t k = 0; k < nblk; k++) {
+		uint32_t w[NW32];
+		if (k < nfull) {
+			const uint8_t *bp = p + (size_t)k * H::BLOCK;
+			Raw<NW32> r;
+			if constexpr (H::GLDS) {
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+				glds_read<NW32, AMODE>(slab, r);
+				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+				if (k + 1 < nfull)
+					glds_issue<NW32, AMODE>(bp + H::BLOCK, slab);
+			} else {
+				issue_block<NW32, AMODE>(bp, r);
+			}
+			finish_block<NW32, AMODE>(bp, r, w);
+		} else if (k == nfull && padtab) {
+			if (sizeof(typename H::word) == 4)
+				compress256_kw<H::ASM>(*reinterpret_cast<uint32_t(*)[8]>(&st),
+				    reinterpret_cast<const uint32_t *>(kw));
+			else
+				compress512_kw(*reinterpret_cast<uint64_t(*)[8]>(&st),
+				    reinterpret_cast<const uint64_t *>(kw));
+			continue;
+		} else if (k == nfull) {
+			tail_block<NW32>(p + (size_t)nfull * H::BLOCK, rem, w);
+			if (!extra) {
+				w[NW32 - 2] = (uint32_t)(bits >> 32);
+				w[NW32 - 1] = (uint32_t)bits;
+			}
+		} else if (extra && k == nfull + 1) {
+#pragma unroll
+			for (int i = 0; i < NW32; i++)
+				w[i] = 0;
+			w[NW32 - 2] = (uint32_t)(bits >> 32);
+			w[NW32 - 1] = (uint32_t)bits;
+		} else {
+			/* HMAC outer: inner digest || 0x80 || 0... || bit count,
+			 * from the outer midstate */
+#pragma unroll
+			for (int i = 0; i < NW32; i++)
+				w[i] = 0;
+			const int dw = digest_words<H>(st, is384, w);
+#pragma unroll
+			for (int i = 12; i < 16; i++)	/* SHA-384 keeps 12 words */
+				if (i >= dw)
+					w[i] = 0;
+			w[dw] = 0x80000000u;
+			const uint64_t obits = (uint64_t)(H::BLOCK + 4 * dw) << 3;
+			w[NW32 - 2] = (uint32_t)(obits >> 32);
+			w[NW32 - 1] = (uint32_t)obits;
+			load_mid<H>(mid, 1, st);
+		}
+		H::compress(st, w);
+	}
+}
+
 /* digest_one for the variable layout: one block loop, and the pad block
  * from the constant table when the wave (SHA-256: kw) or the workgroup
  * (SHA-512: k512_lds) has one. */
@@ -779,6 +1029,11 @@ template <class H, int AMODE, bool PREFETCH = H::PREFETCH>
 __device__ __forceinline__ void var_digest(const uint8_t *p, uint32_t len,
     int is384, const typename H::word *kw, bool padtab, typename H::State &st)
 {
+	if constexpr (H::FLAT) {
+		digest_flat<H, AMODE, false>(p, len, (uint64_t)len << 3, is384, kw,
+		    padtab, nullptr, st);
+		return;
+	}
 	H::init(st, is384);
 	absorb<H, AMODE, PREFETCH>(p, len, st);
 	if (padtab)
@@ -865,44 +1120,6 @@ struct HKey {
 	uint32_t w[NW32];	/* K' as big-endian words */
 };
 
-/* The state as big-endian digest words (SHA*Final's byte order). */
-template <class H>
-__device__ __forceinline__ int digest_words(const typename H::State &st,
-    int is384, uint32_t (&w)[H::NW32])
-{
-	if (sizeof(typename H::word) == 4) {
-#pragma unroll
-		for (int i = 0; i < 8; i++)
-			w[i] = (uint32_t)st[i];
-		return 8;
-	}
-#pragma unroll
-	for (int i = 0; i < 8; i++) {
-		w[2 * i] = hi32((uint64_t)st[i]);
-		w[2 * i + 1] = lo32((uint64_t)st[i]);
-	}
-	return is384 ? 12 : 16;
-}
-
-/* Midstate `which` (0 inner, 1 outer) from LDS into a state. */
-template <class H>
-__device__ __forceinline__ void load_mid(const uint32_t (*mid)[16], int which,
-    typename H::State &st)
-{
-	/* opaque zero: keeps the reads where they are written (not hoisted
-	 * and shared across the address-mode branches) */
-	uint32_t z;
-	asm volatile("s_mov_b32 %0, 0" : "=s"(z));
-	mid += z;
-#pragma unroll
-	for (int i = 0; i < 8; i++) {
-		if (sizeof(typename H::word) == 4)
-			st[i] = mid[which][i];
-		else
-			st[i] = mk64(mid[which][2 * i + 1], mid[which][2 * i]);
-	}
-}
-
 /* Inner hash from the ipad midstate, one address mode. */
 template <class H, int AMODE, bool PADCONST, bool PREFETCH = H::PREFETCH>
 __device__ __forceinline__ void hmac_inner(const uint8_t *p, uint32_t len,
@@ -924,6 +1141,20 @@ __device__ __forceinline__ void hmac_lane(const uint8_t *p, uint32_t len,
     const typename H::word *kw, typename H::State &st, bool padtab = false)
 {
 	constexpr int NW32 = H::NW32;
+	if constexpr (H::FLAT) {
+		const uint64_t bits = ((uint64_t)len + H::BLOCK) << 3;
+		const bool pt = PADCONST || padtab;
+		if (amode == AMODE_A16)
+			digest_flat<H, AMODE_A16, true>(p, len, bits, is384, kw, pt,
+			    mid, st);
+		else if (amode == AMODE_A4)
+			digest_flat<H, AMODE_A4, true>(p, len, bits, is384, kw, pt,
+			    mid, st);
+		else
+			digest_flat<H, AMODE_A1, true>(p, len, bits, is384, kw, pt,
+			    mid, st);
+		return;
+	}
 	/* the midstates stay in LDS and are read where they are used, so
 	 * neither is held in VGPRs across the block loop */
 	if (amode == AMODE_A16)
@@ -982,6 +1213,7 @@ enum { HMAC_DIGESTS = 0, HMAC_SIGN = 1, HMAC_VERIFY = 2, HMAC_BURST_RX = 3,
 #define BURST_VERIFY 0x80u
 #define PKT_PH_ENCRYPTED 0x00000001u	/* types/packet.n2t:27 */
 #define PKT_PH_SIGNED 0x00000002u	/* types/packet.n2t:28 */
+#define PKT_PH_ALTKEY 0x80000000u	/* types/packet.n2t:34 */
 #define PKT_OK 0
 #define PKT_RESOURCE 1
 #define PKT_BAD 2
@@ -1025,7 +1257,7 @@ __device__ __forceinline__ uint32_t load_be32_bytes(const uint8_t *p)
  * three times as much) (profiles/round2/hmac512_waves_ab.txt).
  */
 #ifndef NET2_HMAC512_W5
-#define NET2_HMAC512_W5 0x1
+#define NET2_HMAC512_W5 0x0
 #endif
 /* the same for the SHA-256 HMAC kernels (A/B; 0 = none) */
 #ifndef NET2_HMAC256_W5
@@ -1033,8 +1265,10 @@ __device__ __forceinline__ uint32_t load_be32_bytes(const uint8_t *p)
 #endif
 template <class H, int MODE>
 struct HmacWaves {
-	static constexpr int value = (sizeof(typename H::word) == 8 ?
-	    NET2_HMAC512_W5 : NET2_HMAC256_W5) >> MODE & 1 ? 5 : 1;
+	/* an LDS-DMA kernel's slabs (~35 KB per workgroup) hold it at 4 waves
+	 * per SIMD whatever its VGPRs: no request */
+	static constexpr int value = !H::GLDS && ((sizeof(typename H::word) == 8 ?
+	    NET2_HMAC512_W5 : NET2_HMAC256_W5) >> MODE & 1) ? 5 : 1;
 };
 template <class H, bool PADCONST, int MODE = HMAC_DIGESTS>
 __global__ __launch_bounds__(256)
@@ -1045,7 +1279,9 @@ __attribute__((amdgpu_waves_per_eu(HmacWaves<H, MODE>::value))) void hmac_kernel
     HKey<H::NW32> key, PadKW<typename H::word> pad, BurstArgs rx)
 {
 	constexpr int NW32 = H::NW32;
-	__shared__ uint32_t mid[2][16];
+	/* [0..1]: the key's ipad / opad midstates; [2..3]: the alternate rx
+	 * key's (HMAC_BURST_RX with rx.alt) */
+	__shared__ uint32_t mid[4][16];
 	if (sizeof(typename H::word) == 8) {
 		if (PADCONST)
 			k512_lds_fill_pad(pad);
@@ -1053,25 +1289,28 @@ __attribute__((amdgpu_waves_per_eu(HmacWaves<H, MODE>::value))) void hmac_kernel
 			k512_lds_fill();
 	}
 	if (threadIdx.x < 64) {
-		/* lane 0: K' ^ ipad, lane 1: K' ^ opad -- one compression */
+		/* lane 0: K' ^ ipad, lane 1: K' ^ opad, lanes 2 / 3 the same for
+		 * the alternate key -- one compression */
 		const int pass = threadIdx.x & 1;
+		const bool alt = MODE == HMAC_BURST_RX && (threadIdx.x & 2) != 0;
 		const uint32_t pad = pass ? 0x5c5c5c5cu : 0x36363636u;
 		typename H::State ks;
 		H::init(ks, is384);
 		uint32_t w[NW32];
 #pragma unroll
 		for (int i = 0; i < NW32; i++)
-			w[i] = key.w[i] ^ pad;
+			w[i] = (alt ? rx.altkey[i] : key.w[i]) ^ pad;
 		H::compress(ks, w);
 		materialize<H>(ks);
 		uint32_t kw[NW32];
 		digest_words<H>(ks, 0, kw);
-		if (threadIdx.x < 2)
+		if (threadIdx.x < (MODE == HMAC_BURST_RX && rx.alt ? 4u : 2u))
 #pragma unroll
 			for (int i = 0; i < 16; i++)
-				mid[pass][i] = i < (sizeof(typename H::word) == 4 ? 8 : 16) ? kw[i] : 0u;
+				mid[threadIdx.x][i] = i < (sizeof(typename H::word) == 4 ? 8 : 16) ? kw[i] : 0u;
 	}
 	__syncthreads();
+	const uint32_t (*lmid)[16] = mid;	/* this lane's key */
 
 	const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	const bool live = g < n;
@@ -1120,8 +1359,16 @@ __attribute__((amdgpu_waves_per_eu(HmacWaves<H, MODE>::value))) void hmac_kernel
 			rx_seq = load_be32_bytes(p);
 			rx_fl = load_be32_bytes(p + 4);
 		}
+		/* net2_ck_rx_key (src/conn_keys.c:447-476): the alternate key
+		 * when the datagram says so or lies past the cutoff */
+		const bool use_alt = rx_st == PKT_OK && rx.alt &&
+		    ((rx_fl & PKT_PH_ALTKEY) != 0 || (!rx.no_cutoff &&
+		    rx_seq - rx.rx_start >= rx.cutoff - rx.rx_start));
+		if (use_alt)
+			lmid = mid + 2;
+		const int enc_set = use_alt ? rx.alt_enc_set : rx.enc_set;
 		if (rx_st == PKT_OK && ((rx_fl & PKT_PH_SIGNED) == 0 ||
-		    (rx.enc_set && (rx_fl & PKT_PH_ENCRYPTED) == 0)))
+		    (enc_set && (rx_fl & PKT_PH_ENCRYPTED) == 0)))
 			rx_st = PKT_UNSAFE;
 		if (rx_st == PKT_OK) {
 			rx_st |= BURST_VERIFY;	/* hash field || payload */
@@ -1155,7 +1402,7 @@ __attribute__((amdgpu_waves_per_eu(HmacWaves<H, MODE>::value))) void hmac_kernel
 		if (offsets != nullptr)
 			padtab = block_pad512(live, (uint64_t)len + H::BLOCK);
 	}
-	hmac_lane<H, PADCONST>(p, len, is384, amode, mid,
+	hmac_lane<H, PADCONST>(p, len, is384, amode, lmid,
 	    kw != nullptr ? kw : pad.kw, st, padtab);
 	materialize<H>(st);
 	if (!live)
@@ -1247,7 +1494,19 @@ __global__ __launch_bounds__(64) void job_kernel(const uint8_t *__restrict__ sta
 	} else {
 		H::init(st, is384);
 	}
-	absorb<H, AMODE_A16>(stage + jb.data, jb.nblk * (uint32_t)H::BLOCK, st);
+	/* absorb takes a 32-bit length: a job of 4 GiB or more (nblk up to
+	 * UINT32_MAX blocks) goes through in chunks of whole blocks */
+	{
+		const uint8_t *q = stage + jb.data;
+		uint64_t left = (uint64_t)jb.nblk * H::BLOCK;
+		constexpr uint32_t CHUNK = 0x80000000u;	/* a multiple of BLOCK */
+		while (left > CHUNK) {
+			absorb<H, AMODE_A16>(q, CHUNK, st);
+			q += CHUNK;
+			left -= CHUNK;
+		}
+		absorb<H, AMODE_A16>(q, (uint32_t)left, st);
+	}
 	if (jb.flags & NET2_JOB_HMAC) {
 		/* outer hash: IV, K' ^ opad, inner digest || 0x80 || bit count */
 		uint32_t w[NW32];
@@ -2150,13 +2409,13 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 		PadKW<uint64_t> pad = {};
 		if (padconst) {
 			pad_kw512(ibits, pad);
-			hmac_kernel<Sha512, true><<<grid, 256, 0, s>>>(base, offsets,
+			hmac_kernel<Sha512HF, true><<<grid, 256, 0, s>>>(base, offsets,
 			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad, rx);
 		} else if (offsets != nullptr) {
 			launch_hmac_var_mode<Sha512H>(mode, grid, s, base, offsets,
 			    lens, perm, n, out, dlen, is384, k, pad, rx);
 		} else {
-			hmac_kernel<Sha512, false><<<grid, 256, 0, s>>>(base, offsets,
+			hmac_kernel<Sha512HF, false><<<grid, 256, 0, s>>>(base, offsets,
 			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad, rx);
 		}
 	}

@@ -67,6 +67,14 @@ struct BurstArgs {
 	uint32_t *flags;	/* RX: out; TX: in */
 	uint8_t *status;	/* RX: code | 0x80 (verdict pending); TX: final code */
 	int enc_set;		/* a cipher key is set */
+	/* RX: the connection's alternate rx key (src/conn_keys.c:447-476),
+	 * same hash algorithm; used per datagram when PH_ALTKEY is set or
+	 * seq - rx_start >= cutoff - rx_start (unless no_cutoff) */
+	int alt;
+	int alt_enc_set;
+	int no_cutoff;
+	uint32_t cutoff, rx_start;
+	uint32_t altkey[32];	/* K' as big-endian words */
 };
 hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,

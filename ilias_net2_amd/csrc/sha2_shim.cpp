@@ -1091,38 +1091,77 @@ NET2_EXPORT size_t net2_packet_burst_workspace(uint64_t n)
 	return burst_layout(n, nullptr, nullptr);
 }
 
-NET2_EXPORT int net2_packet_decode_burst(int hash_alg, const void *hash_key,
-    size_t hash_keylen, int enc_alg, uint32_t ivlen, const void *d_base,
-    const uint64_t *d_offsets, const uint32_t *d_lens, uint64_t n,
-    uint8_t *d_result, void *d_iv, uint32_t *d_seq, uint32_t *d_flags,
-    void *d_ws, size_t ws_bytes, void *stream)
+NET2_EXPORT int net2_packet_decode_burst_ck(const struct net2_burst_rx_keys *k,
+    uint32_t ivlen, const void *d_base, const uint64_t *d_offsets,
+    const uint32_t *d_lens, uint64_t n, uint8_t *d_result, void *d_iv,
+    uint32_t *d_seq, uint32_t *d_flags, void *d_ws, size_t ws_bytes,
+    void *stream)
 {
-	int rc = check_burst_args(hash_alg, hash_key, hash_keylen, ivlen, d_base,
-	    d_offsets, d_lens, n, d_result, d_ws, ws_bytes);
-	if (rc != 0 || n == 0)
+	if (k == nullptr)
+		return EINVAL;
+	const int hash_alg = k->hash_alg;
+	int rc = check_burst_args(hash_alg, k->hash_key, k->hash_keylen, ivlen,
+	    d_base, d_offsets, d_lens, n, d_result, d_ws, ws_bytes);
+	if (rc != 0)
 		return rc;
+	/* an alternate key is new key material under the same algorithms */
+	const int hash_set = hash_alg != NET2_HASH_NIL;
+	const bool alt = hash_set && k->alt_hash_key != nullptr;
+	if (alt && k->alt_hash_keylen != k->hash_keylen)
+		return EINVAL;
+	if (n == 0)
+		return 0;
 	if ((d_seq == nullptr) != (d_flags == nullptr))
 		return EINVAL;
 	BurstWs w;
 	burst_layout(n, (uint8_t *)d_ws, &w);
 	uint32_t *seq = d_seq ? d_seq : w.seq, *flags = d_flags ? d_flags : w.flags;
 	hipStream_t s = (hipStream_t)stream;
-	const int hash_set = hash_alg != NET2_HASH_NIL;
+	const int enc_set = k->enc_alg != 0;
 	if (hash_set) {
-		/* header decode, flag checks and HMAC verify in one kernel over
-		 * the wire datagrams (binned by datagram length) */
-		const BurstArgs rx = { seq, flags, w.status, enc_alg != 0 };
-		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)hash_key,
-		    hash_keylen, (const uint8_t *)d_base, d_offsets, d_lens, 0,
+		/* header decode, key choice, flag checks and HMAC verify in one
+		 * kernel over the wire datagrams (binned by datagram length) */
+		BurstArgs rx = {};
+		rx.seq = seq;
+		rx.flags = flags;
+		rx.status = w.status;
+		rx.enc_set = enc_set;
+		if (alt) {
+			const uint8_t *ak = (const uint8_t *)k->alt_hash_key;
+			rx.alt = 1;
+			rx.alt_enc_set = enc_set;
+			rx.no_cutoff = k->alt_no_cutoff != 0;
+			rx.cutoff = k->alt_cutoff;
+			rx.rx_start = k->rx_start;
+			for (size_t i = 0; i < k->alt_hash_keylen; i++)
+				rx.altkey[i / 4] |= (uint32_t)ak[i] << (24 - 8 * (i % 4));
+		}
+		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)k->hash_key,
+		    k->hash_keylen, (const uint8_t *)d_base, d_offsets, d_lens, 0,
 		    0, n, w.verdict, w.bin, s, NET2_HMAC_MODE_BURST_RX, &rx));
 	} else {
 		HIP_TRY(net2_launch_burst_prep((uint8_t *)d_base, d_offsets,
-		    d_lens, n, 0, 0, enc_alg != 0, 0, nullptr, nullptr, seq,
+		    d_lens, n, 0, 0, enc_set, 0, nullptr, nullptr, seq,
 		    flags, w.sub_off, w.sub_len, w.status, s));
 	}
 	HIP_TRY(net2_launch_burst_final(n, w.status, w.verdict, seq, flags,
-	    enc_alg != 0 ? ivlen : 0, (uint8_t *)d_iv, d_result, s));
+	    enc_set ? ivlen : 0, (uint8_t *)d_iv, d_result, s));
 	return 0;
+}
+
+NET2_EXPORT int net2_packet_decode_burst(int hash_alg, const void *hash_key,
+    size_t hash_keylen, int enc_alg, uint32_t ivlen, const void *d_base,
+    const uint64_t *d_offsets, const uint32_t *d_lens, uint64_t n,
+    uint8_t *d_result, void *d_iv, uint32_t *d_seq, uint32_t *d_flags,
+    void *d_ws, size_t ws_bytes, void *stream)
+{
+	struct net2_burst_rx_keys k = {};
+	k.hash_alg = hash_alg;
+	k.hash_key = hash_key;
+	k.hash_keylen = hash_keylen;
+	k.enc_alg = enc_alg;
+	return net2_packet_decode_burst_ck(&k, ivlen, d_base, d_offsets, d_lens,
+	    n, d_result, d_iv, d_seq, d_flags, d_ws, ws_bytes, stream);
 }
 
 NET2_EXPORT int net2_packet_encode_burst(int hash_alg, const void *hash_key,
@@ -1145,8 +1184,11 @@ NET2_EXPORT int net2_packet_encode_burst(int hash_alg, const void *hash_key,
 		/* flag and room checks, header write and HMAC sign in one
 		 * kernel over the wire datagrams; the TX code is final (no
 		 * verdict to fold in), so the kernel writes it to d_result */
-		const BurstArgs tx = { const_cast<uint32_t *>(d_seq),
-		    const_cast<uint32_t *>(d_flags), d_result, enc_alg != 0 };
+		BurstArgs tx = {};
+		tx.seq = const_cast<uint32_t *>(d_seq);
+		tx.flags = const_cast<uint32_t *>(d_flags);
+		tx.status = d_result;
+		tx.enc_set = enc_alg != 0;
 		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)hash_key,
 		    hash_keylen, (const uint8_t *)d_base, d_offsets, d_lens, 0,
 		    0, n, (uint8_t *)d_base, w.bin, s, NET2_HMAC_MODE_BURST_TX,

@@ -84,6 +84,39 @@ int net2_packet_decode_burst(int hash_alg, const void *hash_key,
     void *d_ws, size_t ws_bytes, void *stream);
 
 /*
+ * RX under a connection's full rx key state (src/conn_keys.c): during a key
+ * rollover a datagram may be sealed with the alternate key.  As
+ * net2_ck_rx_key (src/conn_keys.c:447-476) decides for every datagram after
+ * its header is decoded (packet.n2t:210), the kernel verifies datagram i
+ * with the alternate key when alt_hash_key != NULL (an alternate key is
+ * installed, NET2_CK_RX_ALT) and either its flags carry PH_ALTKEY or, unless
+ * alt_no_cutoff (NET2_CK_F_NO_RX_CUTOFF), seq - rx_start >=
+ * alt_cutoff - rx_start (rx_start: the window's cw_rx_start); otherwise with
+ * the active key.  The alternate key is new key material under the same
+ * negotiated algorithms (hash_alg, enc_alg; alt_hash_keylen must equal
+ * hash_keylen).  Everything else as net2_packet_decode_burst, which is this
+ * call with alt_hash_key == NULL.  Committing the alternate key
+ * (net2_ck_rx_key_commit, :487-510) stays with the caller.
+ */
+#define NET2_PH_ALTKEY		0x80000000	/* types/packet.n2t:34 */
+struct net2_burst_rx_keys {
+	int hash_alg;		/* 0 or an HMAC row (4..6) */
+	const void *hash_key;	/* the active key */
+	size_t hash_keylen;
+	int enc_alg;		/* != 0: a cipher key is set */
+	const void *alt_hash_key;	/* NULL: no alternate key */
+	size_t alt_hash_keylen;
+	int alt_no_cutoff;
+	uint32_t alt_cutoff;
+	uint32_t rx_start;
+};
+int net2_packet_decode_burst_ck(const struct net2_burst_rx_keys *keys,
+    uint32_t ivlen, const void *d_base, const uint64_t *d_offsets,
+    const uint32_t *d_lens, uint64_t n, uint8_t *d_result, void *d_iv,
+    uint32_t *d_seq, uint32_t *d_flags, void *d_ws, size_t ws_bytes,
+    void *stream);
+
+/*
  * TX: the hash steps of net2_packet_encode for a burst.  Datagram slot i =
  * d_base[d_offsets[i] .. + d_lens[i]) holds, on entry, 8 bytes for the
  * header, then hashlen reserved bytes when d_flags[i] has PH_SIGNED (as
@@ -92,7 +125,9 @@ int net2_packet_decode_burst(int hash_alg, const void *hash_key,
  * The flags are checked against the keys both ways (NET2_PENCODE_UNSAFE,
  * :364-370); then the header (d_seq[i], d_flags[i]) is written big-endian
  * and, when PH_SIGNED, the HMAC of the payload into the reserved field
- * (:410-443).  A slot too short for header and field gets
+ * (:410-443).  The transmitter picks the key before it builds a datagram
+ * (net2_ck_tx_key, src/conn_keys.c:544-580, sets PH_ALTKEY), so a burst
+ * under the alternate tx key is a call with that key.  A slot too short for header and field gets
  * NET2_PENCODE_RESOURCE and is left untouched.  Codes to d_result.
  */
 int net2_packet_encode_burst(int hash_alg, const void *hash_key,

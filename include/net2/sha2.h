@@ -33,8 +33,24 @@
 #ifndef NET2_SHA2_H
 #define NET2_SHA2_H
 
+#include <sys/types.h>	/* BYTE_ORDER, which src/sha2.c:89-91 requires */
 #include <stddef.h>
 #include <stdint.h>
+
+/*
+ * src/sha2.c marks its definitions ILIAS_NET2_LOCAL (library-internal,
+ * include/ilias/net2/ilias_net2_export.h:32-33), which it takes from this
+ * header's include chain; spelled exactly as there, so the two definitions
+ * agree whichever comes first.  With it, the reference's own src/sha2.c
+ * compiles against this header unchanged (tests/test_ref_headers.py).
+ */
+#ifndef ILIAS_NET2_LOCAL
+#if defined(__GNUC__) || defined(__clang__)
+#define ILIAS_NET2_LOCAL	__attribute__ ((visibility ("hidden")))
+#else
+#define ILIAS_NET2_LOCAL	/* nothing */
+#endif
+#endif
 
 #ifdef __cplusplus
 extern "C" {

@@ -25,6 +25,9 @@ struct net2_sign_ctx;
 /* Number of signature algorithms (1: "ecdsa"), src/sign.c:164-169. */
 extern const int net2_signmax;
 
+/* The ECDSA row (include/ilias/net2/sign.h:61, src/sign.c:653): 0. */
+extern const int net2_sign_ecdsa;
+
 const char *net2_sign_getname(int alg);
 int net2_sign_findname(const char *name);
 

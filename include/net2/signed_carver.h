@@ -59,13 +59,16 @@ struct net2_sc_validate_req {
 /*
  * Handle n carvers' signature steps at once.  Per request rc: 0, EINVAL
  * (bad hash row or arguments), ENOMEM, or the error of the GPU hash / the
- * sign step.  Returns 0, or an errno when the whole batch failed (then
- * every rc carries it too).  nthreads <= 0: one per online CPU, at most 64.
+ * sign step.  Returns 0 when any request succeeded -- the per-request
+ * values are then the outcome, e.g. a SHA-512 group can fail while the
+ * SHA-256 group of the same tick signs -- or, when every request failed,
+ * the first request's error (each rc carries its own).  nthreads <= 0: one per online CPU, at most 64.
  */
 int net2_signed_carver_sign_tick(struct net2_sc_sign_req *reqs, size_t n,
     int nthreads);
 
-/* Handle n combiner checks at once; result per request as above. */
+/* Handle n combiner checks at once; result per request as above (a check
+ * that ran and found the signature invalid, EINVAL, counts as handled). */
 int net2_signed_combiner_validate_tick(struct net2_sc_validate_req *reqs,
     size_t n, int nthreads);
 

@@ -415,8 +415,9 @@ main(int argc, char **argv)
 	pubpem = slurp(argv[2], &publen);
 	if (privpem == NULL || pubpem == NULL)
 		return 2;
-	priv = net2_signctx_privnew(0, privpem, privlen);
-	pub = net2_signctx_pubnew(0, pubpem, publen);
+	/* test/sign.c:66,69 */
+	priv = net2_signctx_privnew(net2_sign_ecdsa, privpem, privlen);
+	pub = net2_signctx_pubnew(net2_sign_ecdsa, pubpem, publen);
 	CHECK(priv != NULL && pub != NULL);
 	CHECK(net2_signctx_pubnew(1, pubpem, publen) == NULL);	/* bad alg */
 	CHECK(net2_signctx_privnew(0, pubpem, publen) == NULL);	/* not priv */

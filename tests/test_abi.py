@@ -158,6 +158,40 @@ def test_no_device_fails_loudly():
     assert L.net2_sha2_ctx_final(1, buf, ctx) == errno.ENODEV
 
 
+@pytest.mark.skipif(_lib.device_count() > 0, reason="a GPU is present")
+@pytest.mark.parametrize("call", ["SHA256Update", "SHA512Final", "SHA256Transform"])
+def test_void_forms_abort_as_last_resort(call):
+    """The reference's void SHA* calls cannot return an error, so a device
+    failure inside one is fatal: it prints why and aborts rather than leave a
+    wrong digest (the documented last resort).  Reference
+    callers are bound to the errno-returning entry points instead, which
+    report the same failure (test_no_device_fails_loudly).  Buffering a
+    partial block needs no device and does not abort.  Fresh process each."""
+    import subprocess
+    import sys
+    code = (
+        "import ctypes, sys\n"
+        "L = ctypes.CDLL(sys.argv[1])\n"
+        "ctx = ctypes.create_string_buffer(208)\n"
+        "L.SHA256Init(ctx); L.SHA512Init(ctx)\n"
+        "L.SHA256Update(ctx, b'x' * 10, ctypes.c_size_t(10))\n"
+        "print('PARTIAL-OK', flush=True)\n"
+        "if sys.argv[2] == 'SHA256Update':\n"
+        "    L.SHA256Init(ctx); L.SHA256Update(ctx, b'x' * 64, ctypes.c_size_t(64))\n"
+        "elif sys.argv[2] == 'SHA512Final':\n"
+        "    L.SHA512Init(ctx); L.SHA512Final(ctypes.create_string_buffer(64), ctx)\n"
+        "else:\n"
+        "    L.SHA256Transform(ctypes.create_string_buffer(32), b'y' * 64)\n"
+        "print('RETURNED', flush=True)\n")
+    r = subprocess.run([sys.executable, "-c", code, _lib.LIB_PATH, call],
+                       capture_output=True, text=True, timeout=300)
+    assert "PARTIAL-OK" in r.stdout, r.stdout + r.stderr
+    assert "RETURNED" not in r.stdout
+    assert r.returncode == -6, (r.returncode, r.stderr)   # SIGABRT
+    assert f"net2: {call} failed on the GPU" in r.stderr, r.stderr
+    assert "cannot report it" in r.stderr
+
+
 def test_missing_library_fails_loudly():
     """No library, no hashing: the binding raises instead of falling back
     to any CPU path (checked in a fresh interpreter)."""

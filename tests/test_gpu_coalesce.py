@@ -286,9 +286,11 @@ print("BAD", bad)
 @pytest.mark.parametrize("mode", ["1", "2"])
 def test_wave_and_lane_job_forms(L, mode):
     """Both kernels behind the coalescer -- one wave per job (the latency
-    form, used up to 1,024 jobs a batch) and one lane per job -- forced in a
-    fresh process each (NET2_COALESCE_JOBMODE), messages up to 70,000 bytes
-    (more than 64 blocks: the wave form's chunk loop)."""
+    form, chosen automatically for batches of up to 16 jobs,
+    kWaveJobsMax in csrc/sha2_coalesce.cpp, or when a job has 1,024 blocks
+    or more, kWaveBlocks) and one lane per job -- forced in a fresh process
+    each (NET2_COALESCE_JOBMODE), messages up to 70,000 bytes (more than 64
+    blocks: the wave form's chunk loop)."""
     import os
     import subprocess
     import sys

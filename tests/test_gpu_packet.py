@@ -9,6 +9,8 @@ payloads and hash fields, and flag / key mismatches (UNSAFE), under each
 key set-up the negotiation can produce (keyed hash and cipher, either one,
 neither).
 """
+import ctypes
+import errno
 import struct
 
 import numpy as np
@@ -191,3 +193,85 @@ def test_burst_argument_errors(dev):
     # an empty burst is a no-op
     assert L.net2_packet_decode_burst(0, None, 0, 0, 0, None, None, None, 0, None,
                                       None, None, None, None, 0, None) == 0
+
+
+def ref_rx_key(seq, fl, has_alt, no_cutoff, cutoff, rx_start):
+    """net2_ck_rx_key (src/conn_keys.c:447-476): True for the alternate
+    key.  u32 wrap-around as in C."""
+    if not has_alt:
+        return False
+    return bool(fl & PH_ALTKEY) or (
+        not no_cutoff and ((seq - rx_start) & 0xffffffff) >=
+        ((cutoff - rx_start) & 0xffffffff))
+
+
+@pytest.mark.parametrize("hash_alg,no_cutoff", [(6, False), (6, True), (4, False), (5, False)])
+def test_decode_burst_alternate_key(dev, oracle_mod, hash_alg, no_cutoff):
+    """A burst received during a key rollover: each datagram sealed with the
+    key net2_ck_rx_key picks for its header (PH_ALTKEY, or a seq past the
+    cutoff, the window start wrapping around), plus datagrams sealed with
+    the other key -- those must come out NET2_PDECODE_BAD, as the
+    reference's hash compare makes them (packet.n2t:226-258)."""
+    from ilias_net2_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(7000 + hash_alg + 10 * no_cutoff)
+    n, hl, ivlen = 2500, HL[hash_alg], 16
+    key = rng.integers(0, 256, hl, dtype=np.uint8).tobytes()
+    alt = rng.integers(0, 256, hl, dtype=np.uint8).tobytes()
+    rx_start = 0xfffff000                     # the window start wraps
+    cutoff = (rx_start + 1200) & 0xffffffff
+    seq = ((rx_start + rng.integers(0, 2500, n)) & 0xffffffff).astype(np.uint32)
+    flags = np.full(n, PH_SIGNED | PH_ENCRYPTED, dtype=np.uint32)
+    flags[rng.random(n) < 0.3] |= PH_ALTKEY
+    wrong = rng.random(n) < 0.1               # sealed with the other key
+    plen = rng.choice([0, 5, 64, 300, 1400], n)
+    dgs, want = [], []
+    for i in range(n):
+        use_alt = ref_rx_key(int(seq[i]), int(flags[i]), True, no_cutoff, cutoff, rx_start)
+        k = (alt if use_alt else key) if not wrong[i] else (key if use_alt else alt)
+        payload = rng.integers(0, 256, int(plen[i]), dtype=np.uint8).tobytes()
+        dgs.append(struct.pack(">II", int(seq[i]), int(flags[i])) +
+                   oracle_mod.hmac(hash_alg, k, payload) + payload)
+        want.append(BAD if wrong[i] else OK)
+    lens = np.array([len(d) for d in dgs], dtype=np.uint32)
+    data, offs = synth.packed(9000 + hash_alg, lens, align=1)
+    for i, d in enumerate(dgs):
+        data[int(offs[i]):int(offs[i]) + len(d)] = np.frombuffer(d, dtype=np.uint8)
+    d = _dev(data, dev)
+    o, ln = _dev(offs.astype(np.int64), dev), _dev(lens.astype(np.int32), dev)
+    res = torch.full((n,), 9, dtype=torch.uint8, device=dev)
+    iv = torch.zeros((n, ivlen), dtype=torch.uint8, device=dev)
+    ws = torch.empty(L.net2_packet_burst_workspace(n), dtype=torch.uint8, device=dev)
+    kb, ab = ctypes.create_string_buffer(key, hl), ctypes.create_string_buffer(alt, hl)
+    ks = _lib.BurstRxKeys(hash_alg, ctypes.cast(kb, ctypes.c_void_p), hl, 1,
+                          ctypes.cast(ab, ctypes.c_void_p), hl, int(no_cutoff),
+                          cutoff, rx_start)
+    st = torch.cuda.current_stream().cuda_stream
+    rc = L.net2_packet_decode_burst_ck(ctypes.byref(ks), ivlen, d.data_ptr(),
+                                       o.data_ptr(), ln.data_ptr(), n, res.data_ptr(),
+                                       iv.data_ptr(), None, None, ws.data_ptr(),
+                                       ws.numel(), st)
+    assert rc == 0
+    got = res.cpu().numpy()
+    giv = iv.cpu().numpy()
+    assert list(got) == want
+    for i in np.nonzero(got == OK)[0][:200]:
+        assert giv[i].tobytes() == oracle_mod.ph_to_iv(int(seq[i]), int(flags[i]), ivlen)
+    # both keys were used, and the plain entry point (no alternate key)
+    # accepts exactly the datagrams sealed with the active key
+    picks = [ref_rx_key(int(seq[i]), int(flags[i]), True, no_cutoff, cutoff, rx_start)
+             for i in range(n)]
+    assert 0 < sum(picks) < n
+    res.fill_(9)
+    rc = L.net2_packet_decode_burst(hash_alg, kb, hl, 1, ivlen, d.data_ptr(),
+                                    o.data_ptr(), ln.data_ptr(), n, res.data_ptr(),
+                                    None, None, None, ws.data_ptr(), ws.numel(), st)
+    assert rc == 0
+    sealed_active = [(not p) != bool(w) for p, w in zip(picks, wrong)]
+    assert list(res.cpu().numpy()) == [OK if s else BAD for s in sealed_active]
+    # the alternate key's length must match the active key's
+    ks.alt_hash_keylen = hl - 1
+    assert L.net2_packet_decode_burst_ck(ctypes.byref(ks), ivlen, d.data_ptr(),
+                                         o.data_ptr(), ln.data_ptr(), n, res.data_ptr(),
+                                         iv.data_ptr(), None, None, ws.data_ptr(),
+                                         ws.numel(), st) == errno.EINVAL

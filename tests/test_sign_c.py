@@ -29,6 +29,12 @@ def test_sign_library_exports():
     for name in (_declared("sign.h") | _declared("signature.h") | _declared("wire.h")
                  | _declared("signed_carver.h")):
         assert hasattr(lib, name), name
+    # the reference's registry constant (include/ilias/net2/sign.h:61,
+    # src/sign.c:653), as test/sign.c:66,69 pass it
+    ecdsa = ctypes.c_int.in_dll(lib, "net2_sign_ecdsa").value
+    assert ecdsa == 0
+    lib.net2_sign_getname.restype = ctypes.c_char_p
+    assert lib.net2_sign_getname(ecdsa) == b"ecdsa"
 
 
 def test_reference_sign_flow_cpu():
