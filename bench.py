@@ -174,10 +174,33 @@ def _time_oracle(run, threads, reps=3):
     return best
 
 
-def cpu_baseline(cfg):
+SHA2C_RATIO = os.path.join(ROOT, "profiles", "round3", "sha2c_ratio.json")
+
+
+def sha2c_ratio():
+    """The port's speed over the reference's own src/sha2.c on identical
+    batches, measured in the build container (tools/sha2c_ratio.sh; the
+    reference tree is not on the GPU box): a labelled constant that turns
+    the box's port figures into src/sha2.c figures."""
+    try:
+        with open(SHA2C_RATIO) as f:
+            summ = json.load(f)["summary"]
+    except (OSError, KeyError, ValueError):
+        return None
+    return {"port_over_sha2c": summ["port_batch_over_sha2c_geomean"],
+            "range": [summ["min"], summ["max"]], "rows": summ["rows"],
+            "source": "profiles/round3/sha2c_ratio.json (tools/sha2c_ratio.sh: "
+                      "src/sha2.c built where it lies with include/net2/sha2.h, "
+                      "C2/C3/C4 batches, rolled and unrolled, 1 and 8 threads, "
+                      "build container; digests identical)"}
+
+
+def cpu_baseline(cfg, light=False):
     """Oracle (clean-room C restatement of src/sha2.c, -O3) on the host
     cores of the GPU box: every usable host CPU (the headline value), the
-    per-GPU share of 16 threads, and one thread."""
+    per-GPU share of 16 threads, and one thread.  light:
+    the 16-thread share in both transform forms and one thread only (the
+    C3 / C4 lines of extra_configs, a few seconds each)."""
     from oracle import oracle
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import synth
@@ -199,7 +222,7 @@ def cpu_baseline(cfg):
     # both transforms of src/sha2.c: rolled (:374-445, the default build)
     # and unrolled (:316-370, SHA2_UNROLL_TRANSFORM)
     t_share = _time_oracle(run, share)
-    t_all = _time_oracle(run, allc, reps=5)
+    t_all = _time_oracle(run, allc, reps=5) if not light else float("inf")
     t_share_u = _time_oracle(lambda t: run(t, n, True), share)
     # one thread, on the first n/16 packets (same shape)
     n1 = max(1, n // 16)
@@ -209,6 +232,21 @@ def cpu_baseline(cfg):
     t0 = time.perf_counter()
     run(1, n1, True)
     single_u = n1 / (time.perf_counter() - t0)
+    ratio = sha2c_ratio()
+    what = cfg["workload"].split(" packets")[0]
+    form_ref = {"rolled": "src/sha2.c:374-445", "unrolled": "src/sha2.c:316-370"}
+    if light:
+        best_t, best_form = min((t_share, "rolled"), (t_share_u, "unrolled"))
+        return {"value": n / best_t, "unit": "digests/s", "cores": share,
+                "kind": "port",
+                "sample": (f"the full {what} packet batch from host memory, "
+                           f"oracle/sha2_oracle.c (-O3, {best_form} transform like "
+                           f"{form_ref[best_form]}) on {share} pthreads (the per-GPU "
+                           f"share), best of 3 after a warm-up"),
+                "rolled_value": n / t_share, "unrolled_value": n / t_share_u,
+                "single_thread_value": max(single, single_u),
+                "reference_sha2c": (dict(ratio, value=round(n / best_t / ratio["port_over_sha2c"], 1))
+                                    if ratio else None)}
     # Context, not the baseline the north star names: the same batch through
     # OpenSSL's SHA*_Init/Update/Final, the calls the reference's C++ layer
     # makes (cxx_src/hash-openssl.cc:25-131; SHA-NI on this host's EPYC).
@@ -223,7 +261,6 @@ def cpu_baseline(cfg):
     t0 = time.perf_counter()
     ossl(1, n1)
     single_ossl = n1 / (time.perf_counter() - t0)
-    what = cfg["workload"].split(" packets")[0]
     topo = _cpu_topology()
     # The headline is the best measured rate.  On the GPU boxes of this pool
     # the process sees every CPU of the node (affinity) but its cgroup
@@ -233,7 +270,6 @@ def cpu_baseline(cfg):
     best_t, best_threads, best_form = min((t_share, share, "rolled"),
                                           (t_all, allc, "rolled"),
                                           (t_share_u, share, "unrolled"))
-    form_ref = {"rolled": "src/sha2.c:374-445", "unrolled": "src/sha2.c:316-370"}
     phys = topo.get("physical_cores")
     return {"value": n / best_t, "unit": "digests/s", "cores": best_threads,
             "kind": "port",
@@ -256,6 +292,10 @@ def cpu_baseline(cfg):
                           "(an estimate, not a measurement; SMT not credited)"}
                 if phys else None),
             "single_thread_value": single,
+            # the reference's own src/sha2.c is not on the GPU box: its rate
+            # here is the port's over the ratio measured in the build container
+            "reference_sha2c": (dict(ratio, value=round(n / best_t / ratio["port_over_sha2c"], 1))
+                                if ratio else None),
             "openssl_context": {
                 "value": n / t_ossl, "threads": share,
                 "single_thread_value": single_ossl,
@@ -298,24 +338,37 @@ def read_sclk(bus):
     return {"max": max(mhz) if mhz else None, "current": cur}
 
 
+def library_build_id():
+    """The kernel build the loaded libnet2_sha2.so was compiled from."""
+    from ilias_net2_amd import _lib
+    return _lib.lib().net2_sha2_build_id().decode()
+
+
 def load_pmc(config_name):
     """Per-launch HBM traffic / VALU counts from the committed rocprofv3 PMC
-    summary (profiles/pmc_<config>.json, written by tools/pmc_summary.py)."""
+    summary (profiles/pmc_<config>.json, written by tools/pmc_summary.py),
+    with whether it was measured on the kernel build that is loaded now
+    (its kernel_build_id stamp)."""
     path = os.path.join(ROOT, "profiles", f"pmc_{config_name}.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     with open(path) as f:
-        return json.load(f)
+        pmc = json.load(f)
+    return pmc, pmc.get("kernel_build_id") == library_build_id()
 
 
 def load_isa_mix(config_name):
     """Instruction mix of the config kernel's block loop, priced with the
-    probed issue costs (profiles/isa_mix.json, written by tools/isa_mix.py)."""
+    probed issue costs (profiles/isa_mix.json, written by tools/isa_mix.py);
+    None unless it was taken from the kernel build that is loaded now."""
     path = os.path.join(ROOT, "profiles", "isa_mix.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
-        return json.load(f)["configs"].get(config_name)
+        mix = json.load(f)
+    if mix.get("kernel_build_id") != library_build_id():
+        return None
+    return mix["configs"].get(config_name)
 
 
 def device_step(name, inp, out, ws_buf, stream, unbinned=False):
@@ -480,12 +533,22 @@ def rooflines(name, launch_ms, per_launch, sclk_mhz=None):
     event-timed launch, PMC traffic from profiles/pmc_<config>.json) and the
     VALU issue figures that bind these kernels."""
     achieved = per_launch / (launch_ms / 1e3) / 1e9
-    pmc = load_pmc(name)
+    pmc, fresh = load_pmc(name)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+            "traffic": None,
             "kernel_ms": round(launch_ms, 4),
             "algorithmic_bytes_per_launch": per_launch}
+    if pmc and not fresh:
+        # counters of another kernel build: not this build's traffic
+        roof["traffic_note"] = (
+            "profiles/pmc_%s.json was measured on kernel build %s, the loaded "
+            "library is %s: counters not reported" % (
+                name, pmc.get("kernel_build_id"), library_build_id()))
+        pmc = None
+    if pmc:
+        roof["traffic"] = pmc.get("hbm_bytes_per_launch")
+        roof["traffic_build_id"] = pmc.get("kernel_build_id")
     if pmc and pmc.get("hbm_bytes_per_launch"):
         roof["traffic_over_algorithmic"] = round(pmc["hbm_bytes_per_launch"] / per_launch, 3)
     valu = None
@@ -654,6 +717,8 @@ def extra_configs(args, dev, probe, ws=1, rank=0):
                      "roofline": roof}
         if valu:
             out[name]["roofline_valu"] = valu
+        if rank == 0 and not args.no_cpu_baseline:
+            out[name]["cpu_baseline"] = cpu_baseline(CONFIGS[name], light=True)
     out["e2e"] = e2e_rate(steps=10, warmup=3)
     out["c1"] = run_c1()
     return out

@@ -48,6 +48,9 @@ _c_u32p = ctypes.POINTER(ctypes.c_uint32)
 # name -> (restype, argtypes)
 SIGNATURES = {
     "net2_sha2_abi_version": (ctypes.c_int, []),
+    "net2_sha2_build_id": (ctypes.c_char_p, []),
+    "net2_sha2_numa_stats": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p]),
     "net2_sha2_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "net2_sha2_last_hip_error": (ctypes.c_int, []),
     "net2_sha2_strerror": (ctypes.c_char_p, [ctypes.c_int]),

@@ -2216,6 +2216,15 @@ static void pad_kw512(uint64_t bits, PadKW<uint64_t> &p)
 
 using namespace net2::dev;
 
+#ifndef NET2_KERNEL_BUILD_ID
+#define NET2_KERNEL_BUILD_ID "unstamped"
+#endif
+extern "C" __attribute__((visibility("default"))) const char *
+net2_sha2_build_id(void)
+{
+	return NET2_KERNEL_BUILD_ID;
+}
+
 static inline unsigned grid_for(uint64_t n)
 {
 	return (unsigned)((n + 255) / 256);

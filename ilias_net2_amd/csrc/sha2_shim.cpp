@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
+#include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
 #include <string.h>
 #include <sys/uio.h>
@@ -340,6 +342,9 @@ struct DeviceCtx {
 	WorkPool *pool = new WorkPool();	/* never freed, see WorkPool */
 	std::mutex mu;		/* one host-memory batch per device at a time */
 	Slot slot[2];
+	/* net2_sha2_numa_stats: slices run, and those whose thread was on
+	 * the device's NUMA node when it finished */
+	std::atomic<uint64_t> slices{0}, slices_on_node{0};
 };
 
 std::mutex g_ctx_mu;
@@ -354,6 +359,120 @@ DeviceCtx *ctx_for(size_t idx)
 		g_ctx[idx].reset(new DeviceCtx());
 	return g_ctx[idx].get();
 }
+
+/*
+ * NUMA placement of a device's host-side work.  A host-memory batch is
+ * sharded over every GPU, one host thread per device (net2_sha2_batch); the
+ * thread packs pageable input into pinned staging, and the staging is
+ * allocated (and first touched) by it.  On a two-socket host half of the
+ * GPUs hang off the other socket, so an unplaced thread pulls its slice's
+ * ~55 GB/s of H2D traffic across the socket link.  The slice thread -- and
+ * the pack pool threads it starts, which inherit its mask -- is bound to the
+ * CPUs of the device's node (sysfs numa_node of its PCI function, within the
+ * process's CPUs) for the slice, and restored after.  NET2_SHA2_NUMA=0
+ * turns it off.
+ */
+struct NumaPlace {
+	int node = -1;
+	bool have = false;	/* cpus holds at least one usable CPU */
+	cpu_set_t cpus;
+};
+
+bool parse_cpulist(const char *s, cpu_set_t *set)
+{
+	CPU_ZERO(set);
+	while (*s && *s != '\n') {
+		char *e;
+		long a = strtol(s, &e, 10), b = a;
+		if (e == s)
+			return false;
+		if (*e == '-') {
+			s = e + 1;
+			b = strtol(s, &e, 10);
+			if (e == s)
+				return false;
+		}
+		for (long c = a; c <= b && c < CPU_SETSIZE; c++)
+			if (c >= 0)
+				CPU_SET((int)c, set);
+		s = *e == ',' ? e + 1 : e;
+	}
+	return true;
+}
+
+const NumaPlace &numa_place(int ordinal)
+{
+	static std::mutex mu;
+	static std::vector<std::unique_ptr<NumaPlace>> cache;
+	std::lock_guard<std::mutex> g(mu);
+	if (cache.size() <= (size_t)ordinal)
+		cache.resize((size_t)ordinal + 1);
+	if (cache[ordinal])
+		return *cache[ordinal];
+	std::unique_ptr<NumaPlace> p(new NumaPlace());
+	CPU_ZERO(&p->cpus);
+	char bus[64] = { 0 }, path[160], buf[4096];
+	if (hipDeviceGetPCIBusId(bus, sizeof(bus) - 1, ordinal) == hipSuccess) {
+		for (char *c = bus; *c; c++)
+			if (*c >= 'A' && *c <= 'F')
+				*c = (char)(*c - 'A' + 'a');
+		snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node",
+		    bus);
+		FILE *f = fopen(path, "r");
+		if (f != nullptr) {
+			if (fscanf(f, "%d", &p->node) != 1)
+				p->node = -1;
+			fclose(f);
+		}
+	} else {
+		(void)hipGetLastError();
+	}
+	if (p->node >= 0) {
+		snprintf(path, sizeof(path),
+		    "/sys/devices/system/node/node%d/cpulist", p->node);
+		FILE *f = fopen(path, "r");
+		cpu_set_t node_cpus, mine;
+		if (f != nullptr && fgets(buf, sizeof(buf), f) != nullptr &&
+		    parse_cpulist(buf, &node_cpus) &&
+		    sched_getaffinity(0, sizeof(mine), &mine) == 0) {
+			CPU_AND(&p->cpus, &node_cpus, &mine);
+			p->have = CPU_COUNT(&p->cpus) > 0;
+		}
+		if (f != nullptr)
+			fclose(f);
+	}
+	cache[ordinal] = std::move(p);
+	return *cache[ordinal];
+}
+
+bool numa_enabled()
+{
+	const char *e = getenv("NET2_SHA2_NUMA");
+	return e == nullptr || strcmp(e, "0") != 0;
+}
+
+/* Binds the calling thread to a device's node for its lifetime. */
+class NumaBind {
+public:
+	explicit NumaBind(const NumaPlace &np)
+	{
+		if (!np.have || !numa_enabled())
+			return;
+		if (pthread_getaffinity_np(pthread_self(), sizeof(saved_),
+		    &saved_) == 0 && pthread_setaffinity_np(pthread_self(),
+		    sizeof(np.cpus), &np.cpus) == 0)
+			bound_ = true;
+	}
+	~NumaBind()
+	{
+		if (bound_)
+			(void)pthread_setaffinity_np(pthread_self(),
+			    sizeof(saved_), &saved_);
+	}
+private:
+	cpu_set_t saved_;
+	bool bound_ = false;
+};
 
 /* Chunk payload target for the host pipeline. */
 constexpr size_t kChunkBytes = 64u << 20;
@@ -584,8 +703,23 @@ int run_device_slice(size_t didx, int ordinal, int alg, const uint8_t *base,
     const uint64_t *offsets, const uint32_t *lens, uint64_t stride,
     uint32_t fixed_len, uint64_t lo, uint64_t hi, uint8_t *digests)
 {
+	/* on the device's node before anything is allocated or touched */
+	const NumaPlace &np = numa_place(ordinal);
+	NumaBind bind(np);
 	DeviceCtx *c = ctx_for(didx);
 	std::lock_guard<std::mutex> g(c->mu);
+	struct Count {
+		DeviceCtx *c;
+		const NumaPlace &np;
+		~Count()
+		{
+			const int cpu = sched_getcpu();
+			c->slices.fetch_add(1, std::memory_order_relaxed);
+			if (np.node >= 0 && cpu >= 0 && CPU_ISSET(cpu, &np.cpus))
+				c->slices_on_node.fetch_add(1,
+				    std::memory_order_relaxed);
+		}
+	} count = { c, np };
 	const int dl = digest_len(alg);
 	int rc = 0, cur = 0;
 
@@ -835,6 +969,25 @@ NET2_EXPORT int net2_sha2_batch(int alg, const void *base,
 	for (int r : rcs)
 		if (r != 0)
 			return r;
+	return 0;
+}
+
+NET2_EXPORT int net2_sha2_numa_stats(int device, int *numa_node,
+    uint64_t *slices, uint64_t *slices_on_node)
+{
+	const std::vector<int> dv = batch_devices();
+	if (dv.empty())
+		return ENODEV;
+	if (device < 0 || (size_t)device >= dv.size())
+		return EINVAL;
+	const NumaPlace &np = numa_place(dv[device]);
+	DeviceCtx *c = ctx_for((size_t)device);
+	if (numa_node)
+		*numa_node = np.node;
+	if (slices)
+		*slices = c->slices.load(std::memory_order_relaxed);
+	if (slices_on_node)
+		*slices_on_node = c->slices_on_node.load(std::memory_order_relaxed);
 	return 0;
 }
 

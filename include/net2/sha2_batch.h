@@ -49,8 +49,28 @@ extern "C" {
 /* ABI version of the loaded library (NET2_SHA2_ABI_VERSION). */
 int net2_sha2_abi_version(void);
 
+/*
+ * Identity of the kernel build: a hash of the kernel sources (plus one of
+ * the -D flags for an A/B build).  Profiles record it next to the counters
+ * they measured (profiles/pmc_*.json), so measurements of another build are
+ * recognisable as such.  A static string.
+ */
+const char *net2_sha2_build_id(void);
+
 /* Number of usable gfx950 devices, via *count.  0 / ENODEV. */
 int net2_sha2_device_count(int *count);
+
+/*
+ * NUMA placement of net2_sha2_batch's host-side work (diagnostics): for
+ * device index `device` of its device list, the NUMA node the GPU hangs
+ * off (-1 when the host does not say), the slices it has run, and how many
+ * of them ended on a CPU of that node (each slice's thread and its pack
+ * threads are bound to the node's CPUs while the slice runs;
+ * NET2_SHA2_NUMA=0 turns that off).  Any pointer may be NULL.  0, EINVAL or
+ * ENODEV.
+ */
+int net2_sha2_numa_stats(int device, int *numa_node, uint64_t *slices,
+    uint64_t *slices_on_node);
 
 /* HIP error code behind the calling thread's last EIO (0 if none). */
 int net2_sha2_last_hip_error(void);

@@ -32,6 +32,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import sys
 import re
 from collections import Counter
 
@@ -237,6 +238,11 @@ def main():
                      "instruction at 2.4 GHz, 8 waves/SIMD)",
            "mixed_stream_source": SEQ_PROBE.replace(ROOT + "/", ""),
            "configs": {}}
+    # the kernel build the asm came from (make asm and the library share
+    # the sources; bench.py ignores the mix of another build)
+    sys.path.insert(0, ROOT)
+    from ilias_net2_amd import _lib
+    res["kernel_build_id"] = _lib.lib().net2_sha2_build_id().decode()
     for cfg, prefix in KERNELS.items():
         res["configs"][cfg] = analyse(lines, prefix, table)
         r = res["configs"][cfg]

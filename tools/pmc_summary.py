@@ -25,6 +25,7 @@ import json
 import os
 import shutil
 import statistics
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = {"c2": "fixed_kernel<net2::dev::Sha256", "c4": "fixed_kernel<net2::dev::Sha512",
@@ -98,6 +99,11 @@ def main():
         res["valu_wave_instr_per_launch"] = med["SQ_INSTS_VALU"]
     if "GRBM_GUI_ACTIVE" in med and durs_all:
         res["clock_ghz_under_pmc"] = med["GRBM_GUI_ACTIVE"] / 8 / statistics.median(durs_all)
+    # the kernel build these counters belong to (bench.py ignores counters
+    # of another build); the library the profiled bench.py runs loaded
+    sys.path.insert(0, ROOT)
+    from ilias_net2_amd import _lib
+    res["kernel_build_id"] = _lib.lib().net2_sha2_build_id().decode()
     out = os.path.join(ROOT, "profiles", f"pmc_{args.cfg}.json")
     with open(out, "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)

@@ -31,7 +31,8 @@ mkdir -p "$(dirname "$OUT")"
     for form in rolled unrolled; do
       for t in 1 $NT; do
         n=$((t == 1 ? 65536 : 262144))
-        row=$($T/ratio_$form $cfg $n $t 5)
+        pin=""; [ $t = 1 ] && pin="taskset -c 2"
+        row=$($pin $T/ratio_$form $cfg $n $t 7)
         [ $first = 1 ] && first=0 || echo ","
         echo "  $row"
       done
@@ -40,9 +41,18 @@ mkdir -p "$(dirname "$OUT")"
   echo "]}"
 } > "$OUT"
 python3 - "$OUT" <<'EOF'
-import json, sys
+import json, math, sys
 d = json.load(open(sys.argv[1]))
 assert all(r["digests_identical"] for r in d["rows"]), "digest mismatch"
+# the constant bench.py quotes: the port's batch entry (what cpu_baseline
+# times) over src/sha2.c, geometric mean over configs, forms, thread counts
+rs = [r["port_batch_over_ref"] for r in d["rows"]]
+d["summary"] = {"port_batch_over_sha2c_geomean": round(math.exp(sum(map(math.log, rs)) / len(rs)), 3),
+                "min": min(rs), "max": max(rs), "rows": len(rs),
+                "note": "spread is the shared build container's noise (alternating best-of-7 timing); "
+                        "both compute identical digests"}
+json.dump(d, open(sys.argv[1], "w"), indent=1)
+print("summary", d["summary"])
 for r in d["rows"]:
     print(f'{r["config"]} {r["form"]:8s} {r["threads"]:3d} thr  sha2.c {r["ref_sha2c_digests_per_s"]/1e6:7.3f} M/s  '
           f'port {r["port_digests_per_s"]/1e6:7.3f} M/s  (batch entry {r["port_batch_digests_per_s"]/1e6:7.3f})  '
