@@ -165,7 +165,11 @@ public:
 	      window_(std::chrono::microseconds(
 		  env_int("NET2_COALESCE_WINDOW_US", 20, 0, 100000))),
 	      zerocopy_(env_int("NET2_COALESCE_ZEROCOPY", 1, 0, 1) != 0),
-	      jobmode_(env_int("NET2_COALESCE_JOBMODE", 0, 0, 2))
+	      jobmode_(env_int("NET2_COALESCE_JOBMODE", 0, 0, 2)),
+	      /* tests only: a small lane-form chunk runs the 4 GiB split on
+	       * small jobs (NET2_COALESCE_JOB_CHUNK, in 128-byte units) */
+	      job_chunk_(128u * (uint32_t)env_int("NET2_COALESCE_JOB_CHUNK",
+		  1 << 24, 1, 1 << 24))
 	{
 		for (int i = nslots_ - 1; i >= 0; i--)
 			free_.push_back(i);
@@ -192,6 +196,7 @@ private:
 	const clk::duration window_;
 	const bool zerocopy_;
 	const int jobmode_;	/* 0 auto, 1 wave per job, 2 lane per job */
+	const uint32_t job_chunk_;
 	int open_ = -1;
 	std::vector<int> free_;
 	int inflight_ = 0;
@@ -540,7 +545,7 @@ int Coalescer::launch_and_wait(Slot &s, int ordinal, int *hip_err)
 	target = s.done_base + waves;
 	CO_TRY(net2_launch_jobs(stage,
 	    reinterpret_cast<const Net2Job *>(stage + hdr_off), (uint32_t)n256,
-	    (uint32_t)(n - n256), d_out, d_done, wave, s.stream));
+	    (uint32_t)(n - n256), d_out, d_done, wave, s.stream, job_chunk_));
 	CO_TRY(hipEventRecord(s.ev, s.stream));
 	{
 		/*

@@ -1474,7 +1474,7 @@ __attribute__((amdgpu_waves_per_eu(HmacWaves<H, MODE>::value))) void hmac_kernel
 template <class H>
 __global__ __launch_bounds__(64) void job_kernel(const uint8_t *__restrict__ stage,
     const Net2Job *__restrict__ jobs, uint32_t n, uint8_t *__restrict__ out,
-    uint32_t *done)
+    uint32_t *done, uint32_t chunk)
 {
 	constexpr int NW32 = H::NW32;
 	typedef typename H::word W;
@@ -1495,15 +1495,15 @@ __global__ __launch_bounds__(64) void job_kernel(const uint8_t *__restrict__ sta
 		H::init(st, is384);
 	}
 	/* absorb takes a 32-bit length: a job of 4 GiB or more (nblk up to
-	 * UINT32_MAX blocks) goes through in chunks of whole blocks */
+	 * UINT32_MAX blocks) goes through in chunks of whole blocks (chunk: a
+	 * multiple of 128 below 4 GiB, 2 GiB unless a test asks for less) */
 	{
 		const uint8_t *q = stage + jb.data;
 		uint64_t left = (uint64_t)jb.nblk * H::BLOCK;
-		constexpr uint32_t CHUNK = 0x80000000u;	/* a multiple of BLOCK */
-		while (left > CHUNK) {
-			absorb<H, AMODE_A16>(q, CHUNK, st);
-			q += CHUNK;
-			left -= CHUNK;
+		while (left > chunk) {
+			absorb<H, AMODE_A16>(q, chunk, st);
+			q += chunk;
+			left -= chunk;
 		}
 		absorb<H, AMODE_A16>(q, (uint32_t)left, st);
 	}
@@ -2432,8 +2432,10 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 }
 hipError_t net2_launch_jobs(const uint8_t *stage, const Net2Job *jobs,
     uint32_t n256, uint32_t n512, uint8_t *out, uint32_t *done, int wave,
-    hipStream_t s)
+    hipStream_t s, uint32_t chunk)
 {
+	if (chunk == 0 || chunk % 128 != 0)
+		return hipErrorInvalidValue;
 	if (wave) {
 		/* one 64-lane workgroup (one wave) per job */
 		if (n256 > 0)
@@ -2447,10 +2449,10 @@ hipError_t net2_launch_jobs(const uint8_t *stage, const Net2Job *jobs,
 	/* 64-lane workgroups: a few jobs spread over as many CUs as waves */
 	if (n256 > 0)
 		job_kernel<Sha256><<<(n256 + 63) / 64, 64, 0, s>>>(stage, jobs,
-		    n256, out, done);
+		    n256, out, done, chunk);
 	if (n512 > 0)
 		job_kernel<Sha512J><<<(n512 + 63) / 64, 64, 0, s>>>(stage,
-		    jobs + n256, n512, out + 64 * (size_t)n256, done);
+		    jobs + n256, n512, out + 64 * (size_t)n256, done, chunk);
 	return hipGetLastError();
 }
 

@@ -105,9 +105,11 @@ struct Net2Job {
  * wave != 0: one wave per job (latency form: the lanes expand the job's
  * blocks in parallel, the wave runs the rounds).
  */
+/* chunk: the lane form absorbs a job in pieces of at most this many bytes
+ * (a multiple of 128; its block loop counts bytes in 32 bits) */
 hipError_t net2_launch_jobs(const uint8_t *stage, const Net2Job *jobs,
     uint32_t n256, uint32_t n512, uint8_t *out, uint32_t *done, int wave,
-    hipStream_t s);
+    hipStream_t s, uint32_t chunk = 0x80000000u);
 
 /*
  * Packet bursts (net2_packet_{encode,decode}_burst): per-datagram header

@@ -283,19 +283,25 @@ print("BAD", bad)
 '''
 
 
-@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("mode", ["1", "2", "2-chunked"])
 def test_wave_and_lane_job_forms(L, mode):
     """Both kernels behind the coalescer -- one wave per job (the latency
     form, chosen automatically for batches of up to 16 jobs,
     kWaveJobsMax in csrc/sha2_coalesce.cpp, or when a job has 1,024 blocks
     or more, kWaveBlocks) and one lane per job -- forced in a fresh process
     each (NET2_COALESCE_JOBMODE), messages up to 70,000 bytes (more than 64
-    blocks: the wave form's chunk loop)."""
+    blocks: the wave form's chunk loop; with 4,096-byte lane-form pieces,
+    the lane form's)."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, NET2_COALESCE_JOBMODE=mode)
+    env = dict(os.environ, NET2_COALESCE_JOBMODE=mode[0])
+    if mode.endswith("chunked"):
+        # the lane form absorbs a job in < 4 GiB pieces (ADVICE round 2: a
+        # 4 GiB job was truncated); 4,096-byte pieces run that split on
+        # these messages (a 4 GiB one would take a lane minutes)
+        env["NET2_COALESCE_JOB_CHUNK"] = "32"
     r = subprocess.run([sys.executable, "-c", _FORM_CHECK], cwd=root, env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
