@@ -46,7 +46,6 @@ struct Sha256T {
 	static constexpr bool PAIR = PAIR_;
 	static constexpr bool DRAIN = DRAIN_;	/* prio_remaining */
 	static constexpr bool GLDS = false;	/* absorb: LDS-DMA staging */
-	static constexpr bool FLAT = false;	/* digest_flat */
 	typedef uint32_t word;
 	static constexpr int BLOCK = 64;	/* bytes per block */
 	static constexpr int NW32 = 16;		/* 32-bit words per block */
@@ -148,7 +147,6 @@ struct Sha512 {
 	/* drain priority (prio_remaining): the fixed kernel only */
 	static constexpr bool DRAIN = NET2_SHA512_DRAIN != 0;
 	static constexpr bool GLDS = false;
-	static constexpr bool FLAT = false;
 	typedef uint64_t word;
 	static constexpr int BLOCK = 128;
 	static constexpr int NW32 = 32;
@@ -194,11 +192,6 @@ struct Sha512 {
 #ifndef NET2_GLDS512
 #define NET2_GLDS512 0x4
 #endif
-/* NET2_FLAT512: the same families with every compression at one call site
- * (digest_flat) */
-#ifndef NET2_FLAT512
-#define NET2_FLAT512 0
-#endif
 /* SHA-512 for the variable-length kernel; NET2_VAR512_PF=1 (A/B only)
  * gives it the two-block ping-pong prefetch the SHA-256 kernels have. */
 #ifndef NET2_VAR512_PF
@@ -207,7 +200,6 @@ struct Sha512 {
 struct Sha512V : Sha512 {
 	static constexpr bool DRAIN = false;
 	static constexpr bool GLDS = (NET2_GLDS512 & 1) != 0;
-	static constexpr bool FLAT = (NET2_FLAT512 & 1) != 0;
 	static constexpr bool U2 = NET2_VAR512_PF != 0 && !GLDS;
 	static constexpr bool PREFETCH = NET2_VAR512_PF != 0 && !GLDS;
 };
@@ -231,14 +223,12 @@ struct Sha512J : Sha512 {
 struct Sha512H : Sha512 {
 	static constexpr bool DRAIN = false;
 	static constexpr bool GLDS = (NET2_GLDS512 & 2) != 0;
-	static constexpr bool FLAT = (NET2_FLAT512 & 2) != 0;
 	static constexpr bool U2 = NET2_HMAC512_PF != 0 && !GLDS;
 	static constexpr bool PREFETCH = NET2_HMAC512_PF != 0 && !GLDS;
 };
 /* ... and for the fixed-layout HMAC-SHA512 kernel (drain priority kept) */
 struct Sha512HF : Sha512 {
 	static constexpr bool GLDS = (NET2_GLDS512 & 4) != 0;
-	static constexpr bool FLAT = (NET2_FLAT512 & 4) != 0;
 };
 
 /* ---- message loading ------------------------------------------------- */
@@ -929,99 +919,6 @@ __device__ __forceinline__ void load_mid(const uint32_t (*mid)[16], int which,
 	}
 }
 
-/*
- * Every compression of one lane's message at one call site (H::FLAT): the
- * data blocks, the tail block (data remainder, 0x80, zero fill, bit count),
- * the zero block SHA*Pad adds when the count does not fit
- * (src/sha2.c:505-519 / :794-808) and, for HMAC, the outer block, each
- * iteration of one loop picking its block.  Spelled out as in
- * absorb + finish + the HMAC outer step, a SHA-512 lane's code holds four
- * or five unrolled compressions of ~28 KB each (five or six with the pad
- * table's); a workgroup's waves run them all at once, well past the
- * instruction cache.  Here the kernel holds one (plus the pad-table form
- * when used).  A wave whose lanes share a length runs the loop in
- * lockstep; binned batches make that the common case.
- *   padtab: the pad block is the whole-block-length constant one, its
- *           K + W schedule at kw (SHA-256) / in k512_lds (SHA-512);
- *   HM:     HMAC -- start from the inner midstate, end with the outer block
- *           from the outer one (mid, as hmac_kernel stages them).
- */
-template <class H, int AMODE, bool HM>
-__device__ __forceinline__ void digest_flat(const uint8_t *p, uint32_t len,
-    uint64_t bits, int is384, const typename H::word *kw, bool padtab,
-    const uint32_t (*mid)[16], typename H::State &st)
-{
-	constexpr int NW32 = H::NW32;
-	const uint32_t nfull = len / H::BLOCK;
-	const uint32_t rem = len % H::BLOCK;
-	const bool extra = !padtab && rem >= (uint32_t)(H::BLOCK - H::LENBYTES);
-	const uint32_t nblk = nfull + 1 + (extra ? 1 : 0) + (HM ? 1 : 0);
-	if (HM)
-		load_mid<H>(mid, 0, st);
-	else
-		H::init(st, is384);
-	uint32_t *slab = nullptr;
-	if constexpr (H::GLDS) {
-		slab = glds_wave_slab();
-		if (nfull > 0)
-			glds_issue<NW32, AMODE>(p, slab);
-	}
-	for (uint32_t k = 0; k < nblk; k++) {
-		uint32_t w[NW32];
-		if (k < nfull) {
-			const uint8_t *bp = p + (size_t)k * H::BLOCK;
-			Raw<NW32> r;
-			if constexpr (H::GLDS) {
-				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-				glds_read<NW32, AMODE>(slab, r);
-				asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-				if (k + 1 < nfull)
-					glds_issue<NW32, AMODE>(bp + H::BLOCK, slab);
-			} else {
-				issue_block<NW32, AMODE>(bp, r);
-			}
-			finish_block<NW32, AMODE>(bp, r, w);
-		} else if (k == nfull && padtab) {
-			if (sizeof(typename H::word) == 4)
-				compress256_kw<H::ASM>(*reinterpret_cast<uint32_t(*)[8]>(&st),
-				    reinterpret_cast<const uint32_t *>(kw));
-			else
-				compress512_kw(*reinterpret_cast<uint64_t(*)[8]>(&st),
-				    reinterpret_cast<const uint64_t *>(kw));
-			continue;
-		} else if (k == nfull) {
-			tail_block<NW32>(p + (size_t)nfull * H::BLOCK, rem, w);
-			if (!extra) {
-				w[NW32 - 2] = (uint32_t)(bits >> 32);
-				w[NW32 - 1] = (uint32_t)bits;
-			}
-		} else if (extra && k == nfull + 1) {
-#pragma unroll
-			for (int i = 0; i < NW32; i++)
-				w[i] = 0;
-			w[NW32 - 2] = (uint32_t)(bits >> 32);
-			w[NW32 - 1] = (uint32_t)bits;
-		} else {
-			/* HMAC outer: inner digest || 0x80 || 0... || bit count,
-			 * from the outer midstate */
-#pragma unroll
-			for (int i = 0; i < NW32; i++)
-				w[i] = 0;
-			const int dw = digest_words<H>(st, is384, w);
-#pragma unroll
-			for (int i = 12; i < 16; i++)	/* SHA-384 keeps 12 words */
-				if (i >= dw)
-					w[i] = 0;
-			w[dw] = 0x80000000u;
-			const uint64_t obits = (uint64_t)(H::BLOCK + 4 * dw) << 3;
-			w[NW32 - 2] = (uint32_t)(obits >> 32);
-			w[NW32 - 1] = (uint32_t)obits;
-			load_mid<H>(mid, 1, st);
-		}
-		H::compress(st, w);
-	}
-}
-
 /* digest_one for the variable layout: one block loop, and the pad block
  * from the constant table when the wave (SHA-256: kw) or the workgroup
  * (SHA-512: k512_lds) has one. */
@@ -1029,11 +926,6 @@ template <class H, int AMODE, bool PREFETCH = H::PREFETCH>
 __device__ __forceinline__ void var_digest(const uint8_t *p, uint32_t len,
     int is384, const typename H::word *kw, bool padtab, typename H::State &st)
 {
-	if constexpr (H::FLAT) {
-		digest_flat<H, AMODE, false>(p, len, (uint64_t)len << 3, is384, kw,
-		    padtab, nullptr, st);
-		return;
-	}
 	H::init(st, is384);
 	absorb<H, AMODE, PREFETCH>(p, len, st);
 	if (padtab)
@@ -1141,20 +1033,6 @@ __device__ __forceinline__ void hmac_lane(const uint8_t *p, uint32_t len,
     const typename H::word *kw, typename H::State &st, bool padtab = false)
 {
 	constexpr int NW32 = H::NW32;
-	if constexpr (H::FLAT) {
-		const uint64_t bits = ((uint64_t)len + H::BLOCK) << 3;
-		const bool pt = PADCONST || padtab;
-		if (amode == AMODE_A16)
-			digest_flat<H, AMODE_A16, true>(p, len, bits, is384, kw, pt,
-			    mid, st);
-		else if (amode == AMODE_A4)
-			digest_flat<H, AMODE_A4, true>(p, len, bits, is384, kw, pt,
-			    mid, st);
-		else
-			digest_flat<H, AMODE_A1, true>(p, len, bits, is384, kw, pt,
-			    mid, st);
-		return;
-	}
 	/* the midstates stay in LDS and are read where they are used, so
 	 * neither is held in VGPRs across the block loop */
 	if (amode == AMODE_A16)
@@ -2215,15 +2093,6 @@ static void pad_kw512(uint64_t bits, PadKW<uint64_t> &p)
 /* ---- launch wrappers (C++ linkage, used by the C-ABI shim) ------------ */
 
 using namespace net2::dev;
-
-#ifndef NET2_KERNEL_BUILD_ID
-#define NET2_KERNEL_BUILD_ID "unstamped"
-#endif
-extern "C" __attribute__((visibility("default"))) const char *
-net2_sha2_build_id(void)
-{
-	return NET2_KERNEL_BUILD_ID;
-}
 
 static inline unsigned grid_for(uint64_t n)
 {

@@ -50,10 +50,11 @@ extern "C" {
 int net2_sha2_abi_version(void);
 
 /*
- * Identity of the kernel build: a hash of the kernel sources (plus one of
- * the -D flags for an A/B build).  Profiles record it next to the counters
- * they measured (profiles/pmc_*.json), so measurements of another build are
- * recognisable as such.  A static string.
+ * Identity of the kernel build: the first 16 hex digits of the SHA-256 of
+ * the kernels' device code (identical machine code, identical id; an A/B
+ * build with other -D flags gets its own).  Profiles record it next to the
+ * counters they measured (profiles/pmc_*.json), so measurements of another
+ * build are recognisable as such.  A static string.
  */
 const char *net2_sha2_build_id(void);
 

@@ -8,12 +8,16 @@ name=$1; shift
 HERE=$(cd "$(dirname "$0")" && pwd)
 SRC=$HERE/../ilias_net2_amd/csrc
 mkdir -p $HERE/ab
-# build id: the in-tree hash of the kernel sources + a hash of the -D flags
-ID=$(cat $SRC/sha2_kernels.hip $SRC/sha2_device.h $SRC/sha2_launch.h | sha256sum | cut -c1-16)+$(echo "$@" | sha256sum | cut -c1-8)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden \
-    -Wall -Wno-unused-result "$@" -DNET2_KERNEL_BUILD_ID="\"$ID\"" -c $SRC/sha2_kernels.hip -o $HERE/ab/$name.o
+    -Wall -Wno-unused-result -cuid=net2sha2 "$@" -c $SRC/sha2_kernels.hip -o $HERE/ab/$name.o
+# build id: hash of the device code, as the Makefile stamps it
+/opt/rocm/lib/llvm/bin/llvm-objcopy --dump-section=.hip_fatbin=$HERE/ab/$name.fatbin \
+    $HERE/ab/$name.o $HERE/ab/$name.tmp.o && rm -f $HERE/ab/$name.tmp.o
+ID=$(sha256sum $HERE/ab/$name.fatbin | cut -c1-16)
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -fvisibility=hidden -DNET2_KERNEL_BUILD_ID="\"$ID\"" \
+    -c $SRC/sha2_buildid.cpp -o $HERE/ab/$name.bid.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $HERE/ab/$name.so \
-    $HERE/ab/$name.o $SRC/build/sha2_shim.o $SRC/build/sha2_coalesce.o \
+    $HERE/ab/$name.o $HERE/ab/$name.bid.o $SRC/build/sha2_shim.o $SRC/build/sha2_coalesce.o \
     $SRC/build/sha2_stream.o -lpthread
-rm -f $HERE/ab/$name.o
-echo built $HERE/ab/$name.so
+rm -f $HERE/ab/$name.o $HERE/ab/$name.bid.o $HERE/ab/$name.fatbin
+echo built $HERE/ab/$name.so "(build id $ID)"
