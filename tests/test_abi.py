@@ -206,3 +206,21 @@ def test_missing_library_fails_loudly():
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=300)
     assert "IMPORTERROR" in r.stdout and "no CPU fallback" in r.stdout, r.stdout + r.stderr
+
+
+def test_build_id_is_the_device_code_hash(tmp_path):
+    """net2_sha2_build_id() -- the stamp profiles/pmc_*.json carry and
+    bench.py checks -- is the SHA-256 (16 hex digits) of the device code
+    actually linked into the library (its .hip_fatbin section)."""
+    import hashlib
+    import shutil
+    import subprocess
+    objcopy = "/opt/rocm/lib/llvm/bin/llvm-objcopy"
+    if not os.path.exists(objcopy):
+        pytest.skip("no llvm-objcopy")
+    fat = tmp_path / "lib.fatbin"
+    subprocess.run([objcopy, f"--dump-section=.hip_fatbin={fat}", _lib.LIB_PATH,
+                    str(tmp_path / "copy.so")], check=True, capture_output=True)
+    want = hashlib.sha256(fat.read_bytes()).hexdigest()[:16]
+    assert _lib.lib().net2_sha2_build_id().decode() == want
+    shutil.rmtree(tmp_path, ignore_errors=True)
