@@ -275,3 +275,78 @@ def test_decode_burst_alternate_key(dev, oracle_mod, hash_alg, no_cutoff):
                                          o.data_ptr(), ln.data_ptr(), n, res.data_ptr(),
                                          iv.data_ptr(), None, None, ws.data_ptr(),
                                          ws.numel(), st) == errno.EINVAL
+
+
+def test_burst_round_trip_full_size(dev, oracle_mod):
+    """The burst bench config at full size (1 M wire datagrams of {136, 584,
+    1500} B, HMAC-SHA512, 16-byte IVs), through properties that do not
+    depend on the size: encode then decode accepts every datagram; each IV
+    equals the device batch net2_ph_to_iv_dev gives for the decoded header;
+    sampled hash fields and IVs equal the oracle's; flipping one payload byte
+    in a chosen set of datagrams makes exactly those NET2_PDECODE_BAD."""
+    from ilias_net2_amd import _lib
+    L = _lib.lib()
+    n, hl, ivlen, alg = 1 << 20, 64, 16, 6
+    g = torch.Generator(device=dev)
+    g.manual_seed(41)
+    choice = torch.tensor([136, 584, 1500], dtype=torch.int64, device=dev)
+    lens = choice[torch.randint(0, 3, (n,), device=dev, generator=g)]
+    offs = torch.zeros(n, dtype=torch.int64, device=dev)
+    offs[1:] = torch.cumsum(lens, 0)[:-1]
+    data = torch.randint(0, 256, (int(lens.sum()),), dtype=torch.uint8,
+                         device=dev, generator=g)
+    l32 = lens.to(torch.int32)
+    seq = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device=dev,
+                        generator=g)
+    flags = torch.full((n,), PH_SIGNED | PH_ENCRYPTED, dtype=torch.int32, device=dev)
+    key = bytes(range(7, 7 + hl))
+    res = torch.full((n,), 9, dtype=torch.uint8, device=dev)
+    ws = torch.empty(L.net2_packet_burst_workspace(n), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    assert L.net2_packet_encode_burst(alg, key, hl, 1, seq.data_ptr(), flags.data_ptr(),
+                                      data.data_ptr(), offs.data_ptr(), l32.data_ptr(),
+                                      n, res.data_ptr(), ws.data_ptr(), ws.numel(), st) == 0
+    assert int((res != OK).sum()) == 0
+
+    def decode(buf):
+        res.fill_(9)
+        iv = torch.zeros((n, ivlen), dtype=torch.uint8, device=dev)
+        oseq = torch.zeros(n, dtype=torch.int32, device=dev)
+        ofl = torch.zeros(n, dtype=torch.int32, device=dev)
+        assert L.net2_packet_decode_burst(alg, key, hl, 1, ivlen, buf.data_ptr(),
+                                          offs.data_ptr(), l32.data_ptr(), n,
+                                          res.data_ptr(), iv.data_ptr(), oseq.data_ptr(),
+                                          ofl.data_ptr(), ws.data_ptr(), ws.numel(),
+                                          st) == 0
+        return res.clone(), iv, oseq, ofl
+
+    got, iv, oseq, ofl = decode(data)
+    assert int((got != OK).sum()) == 0
+    assert torch.equal(oseq, seq) and torch.equal(ofl, flags)
+    want_iv = torch.empty_like(iv)
+    assert L.net2_ph_to_iv_dev(seq.data_ptr(), flags.data_ptr(), n, ivlen,
+                               want_iv.data_ptr(), st) == 0
+    assert torch.equal(iv, want_iv)
+    # a sample against the oracle: the sealed hash field and the IV
+    rng = np.random.default_rng(42)
+    sample = rng.choice(n, 512, replace=False)
+    offs_h, lens_h = offs.cpu().numpy(), lens.cpu().numpy()
+    seq_h = seq.cpu().numpy().view(np.uint32)
+    iv_h = iv.cpu().numpy()
+    for i in sample:
+        a, b = int(offs_h[i]), int(offs_h[i]) + int(lens_h[i])
+        dg = data[a:b].cpu().numpy().tobytes()
+        assert dg[:8] == struct.pack(">II", int(seq_h[i]), PH_SIGNED | PH_ENCRYPTED)
+        assert dg[8:8 + hl] == oracle_mod.hmac(alg, key, dg[8 + hl:]), i
+        assert iv_h[i].tobytes() == oracle_mod.ph_to_iv(
+            int(seq_h[i]), PH_SIGNED | PH_ENCRYPTED, ivlen), i
+    # tamper with a chosen set: exactly those fail the hash compare
+    bad = np.sort(rng.choice(n, 4096, replace=False))
+    pos = offs_h[bad] + 8 + rng.integers(0, lens_h[bad] - 8)
+    t = data.clone()
+    idx = torch.from_numpy(pos.astype(np.int64)).to(dev)
+    t[idx] ^= 0x20
+    got, _, _, _ = decode(t)
+    want = torch.zeros(n, dtype=torch.uint8, device=dev)
+    want[torch.from_numpy(bad.astype(np.int64)).to(dev)] = BAD
+    assert torch.equal(got, want)
