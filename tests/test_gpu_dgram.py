@@ -105,3 +105,39 @@ def test_dgram_argument_errors(dev):
     # empty batches are no-ops
     assert L.net2_hmac_sign_dev(4, key, 32, None, None, None, 0, None, 0,
                                 None) == 0
+
+
+@pytest.mark.parametrize("alg", [4, 6])
+def test_sign_then_verify_full_size(dev, oracle_mod, alg):
+    """The verify bench configs at full size (1 M datagrams, hash field ||
+    {64, 512, 1500 - hashlen} B message), through size-independent
+    properties: sign then verify accepts every datagram, sampled hash fields
+    equal the oracle's HMAC, and one flipped bit in a chosen set of
+    datagrams fails exactly those."""
+    from ilias_net2_amd import batch
+    n, hl = 1 << 20, HL[alg]
+    g = torch.Generator(device=dev)
+    g.manual_seed(50 + alg)
+    choice = torch.tensor([hl + 64, hl + 512, 1500], dtype=torch.int64, device=dev)
+    lens = choice[torch.randint(0, 3, (n,), device=dev, generator=g)]
+    offs = torch.zeros(n, dtype=torch.int64, device=dev)
+    offs[1:] = torch.cumsum(lens, 0)[:-1]
+    d = torch.randint(0, 256, (int(lens.sum()),), dtype=torch.uint8, device=dev,
+                      generator=g)
+    dl = lens.to(torch.int32)
+    key = bytes(synth.random_bytes(90 + alg, hl))
+    batch.hmac_sign_dev(alg, key, d, offs, dl)
+    assert int(batch.hmac_verify_dev(alg, key, d, offs, dl).sum()) == 0
+    rng = np.random.default_rng(60 + alg)
+    offs_h, lens_h = offs.cpu().numpy(), lens.cpu().numpy()
+    for i in rng.choice(n, 512, replace=False):
+        a, b = int(offs_h[i]), int(offs_h[i]) + int(lens_h[i])
+        dg = d[a:b].cpu().numpy().tobytes()
+        assert dg[:hl] == oracle_mod.hmac(alg, key, dg[hl:]), i
+    bad = np.sort(rng.choice(n, 4096, replace=False))
+    pos = offs_h[bad] + rng.integers(0, lens_h[bad])
+    t = d.clone()
+    t[torch.from_numpy(pos.astype(np.int64)).to(dev)] ^= 0x04
+    want = torch.zeros(n, dtype=torch.uint8, device=dev)
+    want[torch.from_numpy(bad.astype(np.int64)).to(dev)] = 1
+    assert torch.equal(batch.hmac_verify_dev(alg, key, t, offs, dl), want)
