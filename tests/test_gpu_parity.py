@@ -570,3 +570,66 @@ def test_graph_capture(dev, batch, oracle_mod):
     want = oracle_mod.batch(1, data.cpu().numpy(), stride=length, length=length, n=n)
     assert np.array_equal(out.cpu().numpy(), want)
     assert np.array_equal(vout.cpu().numpy(), oracle_mod.batch(3, vdata, offsets=offs, lens=lens))
+
+
+def _hmac_by_composition(batch, alg, key, data, offs, lens, n, dev):
+    """RFC 2104 spelled out with the plain digest kernels: inner =
+    H((K' ^ ipad) || m) over a rebuilt variable layout, outer =
+    H((K' ^ opad) || inner) over a fixed one -- a path independent of the
+    HMAC kernel's midstates."""
+    halg = alg - 3
+    blk = 64 if halg == 1 else 128
+    dl = {1: 32, 2: 48, 3: 64}[halg]
+    kp = torch.zeros(blk, dtype=torch.uint8, device=dev)
+    kp[:len(key)] = torch.tensor(list(key), dtype=torch.uint8, device=dev)
+    lens64 = lens.to(torch.int64)
+    total = int(lens64.sum())
+    owner = torch.repeat_interleave(torch.arange(n, device=dev), lens64)
+    start = torch.zeros(n, dtype=torch.int64, device=dev)
+    start[1:] = torch.cumsum(lens64, 0)[:-1]
+    within = torch.arange(total, device=dev) - start[owner]
+    src = offs[owner] + within
+    ioffs = start + blk * torch.arange(n, device=dev)
+    inner_in = torch.empty(total + blk * n, dtype=torch.uint8, device=dev)
+    inner_in[ioffs[owner] + blk + within] = data[src]
+    kpos = (ioffs[:, None] + torch.arange(blk, device=dev)[None, :]).reshape(-1)
+    inner_in[kpos] = (kp ^ 0x36).repeat(n)
+    inner = batch.digest_var(halg, inner_in, ioffs, (lens64 + blk).to(torch.int32))
+    outer_in = torch.cat([(kp ^ 0x5c).repeat(n, 1), inner[:, :dl]], dim=1).contiguous()
+    return batch.digest_fixed(halg, outer_in.reshape(-1), blk + dl, blk + dl, n)
+
+
+@pytest.mark.parametrize("alg", [4, 6])
+@pytest.mark.parametrize("layout", ["fixed_1k", "mtu_mix"])
+def test_hmac_full_size_by_composition(dev, batch, oracle_mod, alg, layout):
+    """The HMAC bench configs at full size (1 M x 1 KiB, 1 M x {64, 512,
+    1500} B): the HMAC kernel against RFC 2104 composed from the plain
+    digest kernels, every digest; a sample against the oracle's HMAC."""
+    n = 1 << 20
+    g = torch.Generator(device=dev)
+    g.manual_seed(70 + alg)
+    if layout == "fixed_1k":
+        lens = torch.full((n,), 1024, dtype=torch.int64, device=dev)
+    else:
+        ch = torch.tensor([64, 512, 1500], dtype=torch.int64, device=dev)
+        lens = ch[torch.randint(0, 3, (n,), device=dev, generator=g)]
+    offs = torch.zeros(n, dtype=torch.int64, device=dev)
+    offs[1:] = torch.cumsum(lens, 0)[:-1]
+    data = torch.randint(0, 256, (int(lens.sum()),), dtype=torch.uint8,
+                         device=dev, generator=g)
+    key = bytes(synth.random_bytes(75 + alg, {4: 32, 6: 64}[alg]))
+    if layout == "fixed_1k":
+        got = batch.hmac_dev(alg, key, data, stride=1024, length=1024, n=n)
+    else:
+        got = batch.hmac_dev(alg, key, data, offsets=offs,
+                             lens=lens.to(torch.int32))
+    want = _hmac_by_composition(batch, alg, key, data, offs,
+                                lens.to(torch.int32), n, dev)
+    assert torch.equal(got, want)
+    rng = np.random.default_rng(80 + alg)
+    offs_h, lens_h = offs.cpu().numpy(), lens.cpu().numpy()
+    got_h = got.cpu().numpy()
+    for i in rng.choice(n, 256, replace=False):
+        a, b = int(offs_h[i]), int(offs_h[i]) + int(lens_h[i])
+        msg = data[a:b].cpu().numpy().tobytes()
+        assert got_h[i].tobytes() == oracle_mod.hmac(alg, key, msg), i
