@@ -406,13 +406,16 @@ def test_config4_full_sha512(dev, batch, oracle_mod):
     _full_fixed(dev, batch, oracle_mod, 3, 5)
 
 
-def test_config3_full_mixed(dev, batch, oracle_mod):
+@pytest.mark.parametrize("alg", [1, 2, 3])
+def test_config3_full_mixed(dev, batch, oracle_mod, alg):
+    """C3 at full size, and the same mix through SHA-384 / SHA-512 (the
+    c3_512 bench config)."""
     n = 1 << 20
     lens = synth.mixed_lengths(3, n)
     data, offs = synth.packed(4, lens)
-    got = batch.digest_var(1, to_dev(data, dev), to_dev(offs.astype(np.int64), dev),
+    got = batch.digest_var(alg, to_dev(data, dev), to_dev(offs.astype(np.int64), dev),
                            to_dev(lens.astype(np.int32), dev)).cpu().numpy()
-    want = oracle_mod.batch(1, data, offsets=offs, lens=lens,
+    want = oracle_mod.batch(alg, data, offsets=offs, lens=lens,
                             nthreads=CPU_THREADS)
     bad = np.nonzero((got != want).any(axis=1))[0]
     assert bad.size == 0, bad[:8]
