@@ -269,3 +269,36 @@ def test_slice_threads_run_on_the_device_numa_node(dev, virtual, oracle_mod):
         if node.value >= 0:      # the host reports the GPU's node
             assert on.value == slices.value, (d, node.value, slices.value, on.value)
     assert L.net2_sha2_numa_stats(3, None, None, None) == 22     # EINVAL
+
+
+def test_config5_full_size_eight_slices(dev, monkeypatch, oracle_mod):
+    """BASELINE configs[4] at full size: 8 M x 1 KiB SHA-256 from pinned host
+    memory through net2_sha2_batch over 8 devices (the one GPU listed 8
+    times: 8 slices of 1 M, each with its own thread, staging and streams, at
+    the default 16 MiB minimum slice), digests straight to pinned host
+    memory; every digest against the oracle."""
+    import ctypes
+    from ilias_net2_amd import _lib
+    monkeypatch.setenv("NET2_SHA2_VIRTUAL_DEVICES", "8")
+    L = _lib.lib()
+    n, length = 8 << 20, 1024
+    g = torch.Generator(device=dev)
+    g.manual_seed(6)
+    src = torch.empty((n * length,), dtype=torch.uint8, pin_memory=True)
+    src.copy_(torch.randint(0, 256, (n * length,), dtype=torch.uint8, device=dev,
+                            generator=g))
+    out = torch.empty((n, 32), dtype=torch.uint8, pin_memory=True)
+    before = []
+    slices = ctypes.c_uint64(0)
+    for d in range(8):
+        assert L.net2_sha2_numa_stats(d, None, ctypes.byref(slices), None) == 0
+        before.append(slices.value)
+    assert L.net2_sha2_batch(1, src.data_ptr(), None, None, length, length, n,
+                             out.data_ptr(), 0) == 0
+    want = oracle_mod.batch(1, src.numpy(), stride=length, length=length, n=n,
+                            nthreads=CPU_THREADS)
+    assert _bad(out.numpy(), want).size == 0, _bad(out.numpy(), want)
+    # one slice per virtual device
+    for d in range(8):
+        assert L.net2_sha2_numa_stats(d, None, ctypes.byref(slices), None) == 0
+        assert slices.value == before[d] + 1, d
