@@ -546,6 +546,87 @@ def test_concurrent_host_threads(dev, H, oracle_mod):
     assert not errors, errors[:5]
 
 
+def test_concurrent_streams_device_paths(dev, batch, oracle_mod):
+    """Device-resident batches submitted from several host threads at once,
+    each on its own stream with its own workspace and outputs (the way a
+    multi-stream caller overlaps batches): binned variable-length digests,
+    HMAC over a fixed layout and a packet burst round trip, ten times each
+    per thread, every result checked."""
+    import ctypes
+    import threading
+    from ilias_net2_amd import _lib
+    L = _lib.lib()
+    n = 20000
+    jobs = []
+    for t in range(4):
+        lens = synth.mixed_lengths(900 + t, n)
+        data, offs = synth.packed(910 + t, lens, align=1 + 3 * (t % 2))
+        alg = 1 + t % 3
+        fdata = synth.fixed_batch(920 + t, n, 700)
+        key = bytes(synth.random_bytes(930 + t, 64))
+        jobs.append(dict(
+            alg=alg, vd=to_dev(data, dev), vo=to_dev(offs.astype(np.int64), dev),
+            vl=to_dev(lens.astype(np.int32), dev),
+            want_v=oracle_mod.batch(alg, data, offsets=offs, lens=lens,
+                                    nthreads=CPU_THREADS),
+            fd=to_dev(fdata, dev), key=key,
+            want_h=np.stack([np.frombuffer(oracle_mod.hmac(
+                6, key, fdata[i * 700:(i + 1) * 700].tobytes()), dtype=np.uint8)
+                for i in range(0, n, 97)])))
+    errors = []
+
+    def worker(t):
+        try:
+            j = jobs[t]
+            s = torch.cuda.Stream(dev)
+            ws = batch.var_workspace(n, dev, stream=s)
+            bws = torch.empty(L.net2_packet_burst_workspace(n), dtype=torch.uint8,
+                              device=dev)
+            for r in range(10):
+                with torch.cuda.stream(s):
+                    got = batch.digest_var(j["alg"], j["vd"], j["vo"], j["vl"],
+                                           workspace=ws, stream=s)
+                    hm = batch.hmac_dev(6, j["key"], j["fd"], stride=700,
+                                        length=700, n=n, stream=s)
+                    # burst: seal a copy of the variable batch, then open it
+                    d = j["vd"].clone()
+                    seq = torch.arange(n, dtype=torch.int32, device=dev) + r
+                    fl = torch.full((n,), 3, dtype=torch.int32, device=dev)
+                    res = torch.full((n,), 9, dtype=torch.uint8, device=dev)
+                    rc1 = L.net2_packet_encode_burst(
+                        6, j["key"], 64, 1, seq.data_ptr(), fl.data_ptr(),
+                        d.data_ptr(), j["vo"].data_ptr(), j["vl"].data_ptr(), n,
+                        res.data_ptr(), bws.data_ptr(), bws.numel(), s.cuda_stream)
+                    enc = res.clone()
+                    rc2 = L.net2_packet_decode_burst(
+                        6, j["key"], 64, 1, 0, d.data_ptr(), j["vo"].data_ptr(),
+                        j["vl"].data_ptr(), n, res.data_ptr(), None, None, None,
+                        bws.data_ptr(), bws.numel(), s.cuda_stream)
+                s.synchronize()
+                if rc1 or rc2:
+                    errors.append(("rc", t, r, rc1, rc2))
+                if not np.array_equal(got.cpu().numpy(), j["want_v"]):
+                    errors.append(("var", t, r))
+                if not np.array_equal(hm.cpu().numpy()[::97], j["want_h"]):
+                    errors.append(("hmac", t, r))
+                # every slot with room seals (the 64-byte ones have none for
+                # header and hash field), and every sealed one opens
+                room = j["vl"] >= 8 + 64
+                if not (torch.equal(enc[room], torch.zeros_like(enc[room])) and
+                        bool((enc[~room] == 1).all()) and
+                        torch.equal(res[room], enc[room])):
+                    errors.append(("burst", t, r))
+        except Exception as e:  # noqa: BLE001
+            errors.append(("exc", t, repr(e)))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errors, errors[:5]
+
+
 def test_graph_capture(dev, batch, oracle_mod):
     """The device entry points allocate and synchronise nothing, so a batch
     launch can be captured into a hipGraph and replayed."""
