@@ -307,7 +307,10 @@ int Coalescer::submit(int ordinal, const Request &r, int *hip_err)
 	}
 	const size_t need = align64(body + aux);
 	const size_t nblk = body / blk;
-	if (nblk > UINT32_MAX)
+	/* the wave form walks a job in 64-block steps of a 32-bit block index:
+	 * keep its last step below 2^32 (a job of 2^32 - 64 blocks is 256 GiB
+	 * of SHA-256, 512 GiB of SHA-512) */
+	if (nblk > UINT32_MAX - 64)
 		return EINVAL;
 
 	Job job;
