@@ -38,6 +38,7 @@
 
 #include "../../include/net2/hash.h"
 #include "../../include/net2/packet.h"
+#include "../../include/net2/sha2.h"
 
 namespace {
 
@@ -1016,6 +1017,61 @@ NET2_EXPORT int net2_hash_getkeylen(int alg)
 	return alg >= 0 && alg < kNumRows ? kRows[alg].keylen : -1;
 }
 
+/*
+ * A message longer than this (NET2_SHA2_STREAM_CHUNK, default 64 MiB) is
+ * hashed through the streaming context, whose Update sends it in requests
+ * of at most that size: one request would stage the whole message in
+ * page-locked memory.
+ */
+static size_t long_message_bytes()
+{
+	const char *e = getenv("NET2_SHA2_STREAM_CHUNK");
+	return e != nullptr && *e != '\0' ? strtoull(e, nullptr, 10) :
+	    (size_t)64 << 20;
+}
+
+/* net2_hashctx_hashiov of a long message: SHA*Init / Update per segment /
+ * Final, and for HMAC the same over K' ^ ipad || m, then K' ^ opad || inner
+ * (RFC 2104, as hash-openssl.cc's HMAC_* calls). */
+static int hashiov_streamed(int alg, const void *key, size_t keylen,
+    const struct iovec *iov, size_t iovcnt, uint8_t *out)
+{
+	const bool keyed = !unkeyed_sha2(alg);
+	const int halg = keyed ? alg - 3 : alg;
+	const size_t B = halg == NET2_HASH_SHA256 ? 64 : 128;
+	uint8_t kp[128] = { 0 }, blk[128], inner[64];
+	SHA2_CTX c;
+	int rc;
+	if (keyed) {
+		if (keylen > B)
+			return EINVAL;
+		memcpy(kp, key, keylen);
+	}
+	if ((rc = net2_sha2_ctx_init(halg, &c)) != 0)
+		return rc;
+	if (keyed) {
+		for (size_t i = 0; i < B; i++)
+			blk[i] = kp[i] ^ 0x36;
+		if ((rc = net2_sha2_ctx_update(halg, &c, blk, B)) != 0)
+			return rc;
+	}
+	for (size_t i = 0; i < iovcnt; i++)
+		if ((rc = net2_sha2_ctx_update(halg, &c, iov[i].iov_base,
+		    iov[i].iov_len)) != 0)
+			return rc;
+	if ((rc = net2_sha2_ctx_final(halg, keyed ? inner : out, &c)) != 0 ||
+	    !keyed)
+		return rc;
+	for (size_t i = 0; i < B; i++)
+		blk[i] = kp[i] ^ 0x5c;
+	if ((rc = net2_sha2_ctx_init(halg, &c)) != 0 ||
+	    (rc = net2_sha2_ctx_update(halg, &c, blk, B)) != 0 ||
+	    (rc = net2_sha2_ctx_update(halg, &c, inner,
+	    (size_t)kRows[alg].hashlen)) != 0)
+		return rc;
+	return net2_sha2_ctx_final(halg, out, &c);
+}
+
 NET2_EXPORT int net2_hashctx_hashiov(int alg, const void *key, size_t keylen,
     const struct iovec *iov, size_t iovcnt, void *out, size_t outlen)
 {
@@ -1030,6 +1086,12 @@ NET2_EXPORT int net2_hashctx_hashiov(int alg, const void *key, size_t keylen,
 		return 0;
 	if (out == nullptr || outlen < (size_t)kRows[alg].hashlen)
 		return EINVAL;
+	size_t total = 0;
+	for (size_t i = 0; i < iovcnt; i++)
+		total += iov[i].iov_len;
+	if (total > long_message_bytes())
+		return hashiov_streamed(alg, key, keylen, iov, iovcnt,
+		    (uint8_t *)out);
 	/* one coalesced request: concurrent callers share a launch */
 	net2co::Request r = {};
 	r.kind = unkeyed_sha2(alg) ? net2co::DIGEST : net2co::HMAC;

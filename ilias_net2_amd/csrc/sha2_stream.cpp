@@ -39,21 +39,63 @@ void add_bits(int alg, SHA2_CTX *c, uint64_t nbits)
 		c->bitcount[1]++;
 }
 
-/* state = compress(state, the whole blocks of v[0 .. nv)); all or nothing */
+/*
+ * Bytes per coalesced request of one Update: a long Update goes through in
+ * requests of at most this many bytes, so the coalescer's page-locked
+ * staging stays bounded (NET2_SHA2_STREAM_CHUNK, read per call, in bytes,
+ * rounded down to whole blocks; tests shrink it).
+ */
+size_t stream_chunk(size_t B)
+{
+	const char *e = getenv("NET2_SHA2_STREAM_CHUNK");
+	size_t c = e != nullptr && *e != '\0' ? strtoull(e, nullptr, 10) :
+	    (size_t)64 << 20;
+	return std::max(c / B * B, B);
+}
+
+/*
+ * state = compress(state, the whole blocks of v[0 .. nv)); all or nothing:
+ * the chunks chain through a local state, committed when the last is done.
+ */
 int compress(int alg, void *state, const struct iovec *v, size_t nv)
 {
-	uint8_t next[64];
-	net2co::Request r = {};
-	r.kind = net2co::BLOCKS;
-	r.alg = alg;
-	r.iov = v;
-	r.iovcnt = nv;
-	r.state = state;
-	r.out = next;
-	const int rc = net2_co_run(r);
-	if (rc == 0)
-		memcpy(state, next, alg == 1 ? 32 : 64);
-	return rc;
+	const size_t B = block_of(alg), S = alg == 1 ? 32 : 64;
+	const size_t chunk = stream_chunk(B);
+	uint8_t cur[64], next[64];
+	struct iovec part[8];
+	size_t i = 0, off = 0;
+	memcpy(cur, state, S);
+	while (i < nv) {
+		/* up to `chunk` bytes of v, from v[i] + off */
+		size_t np = 0, bytes = 0;
+		while (i < nv && np < 8 && bytes < chunk) {
+			const size_t take = std::min(v[i].iov_len - off, chunk - bytes);
+			if (take != 0)
+				part[np++] = { static_cast<uint8_t *>(v[i].iov_base) +
+				    off, take };
+			bytes += take;
+			off += take;
+			if (off == v[i].iov_len) {
+				i++;
+				off = 0;
+			}
+		}
+		if (bytes == 0)
+			continue;
+		net2co::Request r = {};
+		r.kind = net2co::BLOCKS;
+		r.alg = alg;
+		r.iov = part;
+		r.iovcnt = np;
+		r.state = cur;
+		r.out = next;
+		const int rc = net2_co_run(r);
+		if (rc != 0)
+			return rc;
+		memcpy(cur, next, S);
+	}
+	memcpy(state, cur, S);
+	return 0;
 }
 
 void fatal(const char *what, int rc)

@@ -68,6 +68,31 @@ def test_streaming_matches_oracle_call_by_call(L, oracle_mod):
             assert c.raw == oc.raw == b"\0" * 208
 
 
+def test_long_update_in_chunks(L, oracle_mod, monkeypatch):
+    """An Update longer than the per-request chunk goes through in several
+    coalesced requests chained through a local state (small chunks forced
+    with NET2_SHA2_STREAM_CHUNK): the context matches the oracle's after
+    every call, whatever the chunk and the buffered head."""
+    O = oracle_mod.lib()
+    rng = np.random.default_rng(3)
+    for chunk in ("64", "4096", "65600"):
+        monkeypatch.setenv("NET2_SHA2_STREAM_CHUNK", chunk)
+        for alg in (1, 2, 3):
+            p, op = PFX[alg], OPFX[alg]
+            m = rng.integers(0, 256, 300001, dtype=np.uint8).tobytes()
+            c, oc = _ctx(), _ctx()
+            getattr(L, p + "Init")(c)
+            getattr(O, f"oracle_{op}_init")(oc)
+            for ch in (m[:13], m[13:250013], m[250013:]):
+                b = _buf(ch)
+                getattr(L, p + "Update")(c, b, len(ch))
+                getattr(O, f"oracle_{op}_update")(oc, b, len(ch))
+                assert c.raw == oc.raw, (chunk, alg, len(ch))
+            d = ctypes.create_string_buffer(64)
+            getattr(L, p + "Final")(d, c)
+            assert d.raw[:DL[alg]] == oracle_mod.digest(alg, m), (chunk, alg)
+
+
 def test_pad_and_final_null(L, oracle_mod):
     """Pad alone, and Final(NULL) keeping the padded context for SHA-256 /
     SHA-512 while SHA-384 zeroes it (src/sha2.c:551-562, :918)."""
@@ -122,6 +147,36 @@ def test_hashiov_sizes(L, oracle_mod):
         for alg in (4, 5, 6):
             key = bytes(range(DL[alg - 3]))
             assert h.hashbuf(alg, key, m) == oracle_mod.hmac(alg, key, m), (alg, n)
+
+
+def test_hashiov_long_messages_streamed(L, oracle_mod, monkeypatch):
+    """A message longer than NET2_SHA2_STREAM_CHUNK (64 MiB by default; 4 KiB
+    here) goes through the streaming context in chunks instead of one
+    request, keyed rows as RFC 2104 over it: every row, segments of odd
+    sizes, against the oracle; the threshold itself takes the one-request
+    path."""
+    import ctypes as ct
+    monkeypatch.setenv("NET2_SHA2_STREAM_CHUNK", "4096")
+    rng = np.random.default_rng(5)
+    for n in (4096, 4097, 100003):
+        m = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        cuts = sorted(rng.integers(0, n + 1, 4).tolist())
+        segs = [m[a:b] for a, b in zip([0] + cuts, cuts + [n])]
+        bufs = [ct.create_string_buffer(x, max(len(x), 1)) for x in segs]
+
+        from ilias_net2_amd._lib import IOVec
+        iov = (IOVec * len(segs))(*[IOVec(ct.cast(b, ct.c_void_p), len(x))
+                                    for b, x in zip(bufs, segs)])
+        for alg in range(1, 7):
+            dl = DL[alg if alg <= 3 else alg - 3]
+            key = bytes(range(dl)) if alg > 3 else b""
+            kb = ct.create_string_buffer(key, max(len(key), 1))
+            out = ct.create_string_buffer(64)
+            assert L.net2_hashctx_hashiov(alg, kb if key else None, len(key), iov,
+                                          len(segs), out, 64) == 0
+            want = oracle_mod.digest(alg, m) if alg <= 3 else \
+                oracle_mod.hmac(alg, key, m)
+            assert out.raw[:dl] == want, (alg, n)
 
 
 def _registry_key(key: bytes, alg: int) -> bytes:
