@@ -90,7 +90,7 @@ SIGNATURES = {
         ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
         ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
-    "net2_ph_to_iv": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t,
+    "net2_ph_to_iv_buf": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t,
                                       ctypes.c_void_p]),
     "net2_ph_to_iv_dev": (ctypes.c_int, [
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,

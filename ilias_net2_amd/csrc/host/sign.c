@@ -24,7 +24,7 @@
 
 #define NET2_EXPORT __attribute__((visibility("default")))
 
-struct net2_sign_ctx {
+struct net2x_sign_ctx {
 	int		 alg;
 	EVP_PKEY	*pkey;
 	int		 is_private;
@@ -37,38 +37,38 @@ struct net2_sign_ctx {
 
 static const char *const sign_names[] = { "ecdsa" };
 
-NET2_EXPORT const int net2_signmax =
+NET2_EXPORT const int net2x_signmax =
     (int)(sizeof(sign_names) / sizeof(sign_names[0]));
 
 /* The ECDSA row of the registry, by name (src/sign.c:653; test/sign.c:66,69
- * pass it to net2_signctx_{priv,pub}new). */
-NET2_EXPORT const int net2_sign_ecdsa = 0;
+ * pass it to net2x_signctx_{priv,pub}new). */
+NET2_EXPORT const int net2x_sign_ecdsa = 0;
 
 NET2_EXPORT const char *
-net2_sign_getname(int alg)
+net2x_sign_getname(int alg)
 {
-	return alg >= 0 && alg < net2_signmax ? sign_names[alg] : NULL;
+	return alg >= 0 && alg < net2x_signmax ? sign_names[alg] : NULL;
 }
 
 NET2_EXPORT int
-net2_sign_findname(const char *name)
+net2x_sign_findname(const char *name)
 {
 	if (name == NULL)
 		return -1;
-	for (int i = 0; i < net2_signmax; i++)
+	for (int i = 0; i < net2x_signmax; i++)
 		if (strcmp(sign_names[i], name) == 0)
 			return i;
 	return -1;
 }
 
-static struct net2_sign_ctx *
+static struct net2x_sign_ctx *
 ctx_from_pem(int alg, const void *key, size_t keylen, int priv)
 {
-	struct net2_sign_ctx *s;
+	struct net2x_sign_ctx *s;
 	EVP_PKEY *pk;
 	BIO *bio;
 
-	if (alg < 0 || alg >= net2_signmax || key == NULL || keylen == 0 ||
+	if (alg < 0 || alg >= net2x_signmax || key == NULL || keylen == 0 ||
 	    keylen > INT32_MAX)
 		return NULL;
 	if ((bio = BIO_new_mem_buf(key, (int)keylen)) == NULL)
@@ -93,20 +93,20 @@ ctx_from_pem(int alg, const void *key, size_t keylen, int priv)
 	return s;
 }
 
-NET2_EXPORT struct net2_sign_ctx *
-net2_signctx_pubnew(int alg, const void *key, size_t keylen)
+NET2_EXPORT struct net2x_sign_ctx *
+net2x_signctx_pubnew(int alg, const void *key, size_t keylen)
 {
 	return ctx_from_pem(alg, key, keylen, 0);
 }
 
-NET2_EXPORT struct net2_sign_ctx *
-net2_signctx_privnew(int alg, const void *key, size_t keylen)
+NET2_EXPORT struct net2x_sign_ctx *
+net2x_signctx_privnew(int alg, const void *key, size_t keylen)
 {
 	return ctx_from_pem(alg, key, keylen, 1);
 }
 
 NET2_EXPORT void
-net2_signctx_free(struct net2_sign_ctx *s)
+net2x_signctx_free(struct net2x_sign_ctx *s)
 {
 	if (s == NULL)
 		return;
@@ -116,10 +116,10 @@ net2_signctx_free(struct net2_sign_ctx *s)
 	free(s);
 }
 
-NET2_EXPORT struct net2_sign_ctx *
-net2_signctx_clone(struct net2_sign_ctx *o)
+NET2_EXPORT struct net2x_sign_ctx *
+net2x_signctx_clone(struct net2x_sign_ctx *o)
 {
-	struct net2_sign_ctx *s;
+	struct net2x_sign_ctx *s;
 
 	if (o == NULL || (s = calloc(1, sizeof(*s))) == NULL)
 		return NULL;
@@ -141,19 +141,19 @@ net2_signctx_clone(struct net2_sign_ctx *o)
 }
 
 NET2_EXPORT size_t
-net2_signctx_maxmsglen(struct net2_sign_ctx *s)
+net2x_signctx_maxmsglen(struct net2x_sign_ctx *s)
 {
 	return s == NULL ? 0 : (size_t)EVP_PKEY_get_size(s->pkey);
 }
 
 NET2_EXPORT const char *
-net2_signctx_name(struct net2_sign_ctx *s)
+net2x_signctx_name(struct net2x_sign_ctx *s)
 {
 	return s == NULL ? NULL : sign_names[s->alg];
 }
 
 NET2_EXPORT int
-net2_signctx_sign(struct net2_sign_ctx *s, const void *in, size_t inlen,
+net2x_signctx_sign(struct net2x_sign_ctx *s, const void *in, size_t inlen,
     void *sig, size_t *siglen)
 {
 	EVP_PKEY_CTX *pc;
@@ -163,7 +163,7 @@ net2_signctx_sign(struct net2_sign_ctx *s, const void *in, size_t inlen,
 		return EINVAL;
 	if (!s->is_private)
 		return EINVAL;
-	if (*siglen < net2_signctx_maxmsglen(s))
+	if (*siglen < net2x_signctx_maxmsglen(s))
 		return EINVAL;
 	if ((pc = EVP_PKEY_CTX_new(s->pkey, NULL)) == NULL)
 		return ENOMEM;
@@ -175,7 +175,7 @@ net2_signctx_sign(struct net2_sign_ctx *s, const void *in, size_t inlen,
 }
 
 NET2_EXPORT int
-net2_signctx_validate(struct net2_sign_ctx *s, const void *sig,
+net2x_signctx_validate(struct net2x_sign_ctx *s, const void *sig,
     size_t siglen, const void *in, size_t inlen)
 {
 	EVP_PKEY_CTX *pc;
@@ -183,7 +183,7 @@ net2_signctx_validate(struct net2_sign_ctx *s, const void *sig,
 
 	if (s == NULL || in == NULL || sig == NULL)
 		return 0;
-	if (siglen > net2_signctx_maxmsglen(s))	/* src/sign.c:527-529 */
+	if (siglen > net2x_signctx_maxmsglen(s))	/* src/sign.c:527-529 */
 		return 0;
 	if ((pc = EVP_PKEY_CTX_new(s->pkey, NULL)) == NULL)
 		return 0;
@@ -195,7 +195,7 @@ net2_signctx_validate(struct net2_sign_ctx *s, const void *sig,
 
 /* Uncompressed EC point of the key, computed once. */
 static int
-pubkey_cached(struct net2_sign_ctx *s)
+pubkey_cached(struct net2x_sign_ctx *s)
 {
 	const EC_KEY *ek;
 	const EC_GROUP *g;
@@ -225,7 +225,7 @@ pubkey_cached(struct net2_sign_ctx *s)
 }
 
 NET2_EXPORT int
-net2_signctx_pubkey(struct net2_sign_ctx *s, void *out, size_t *outlen)
+net2x_signctx_pubkey(struct net2x_sign_ctx *s, void *out, size_t *outlen)
 {
 	int rc;
 
@@ -245,7 +245,7 @@ net2_signctx_pubkey(struct net2_sign_ctx *s, void *out, size_t *outlen)
 }
 
 NET2_EXPORT int
-net2_signctx_fingerprint(struct net2_sign_ctx *s, uint8_t out[32])
+net2x_signctx_fingerprint(struct net2x_sign_ctx *s, uint8_t out[32])
 {
 	struct iovec iov;
 	int rc;

@@ -33,7 +33,7 @@ dupstr(const char *s)
 }
 
 NET2_EXPORT void
-net2_signature_deinit(struct net2_signature *s)
+net2x_signature_deinit(struct net2x_signature *s)
 {
 	if (s == NULL)
 		return;
@@ -48,31 +48,31 @@ net2_signature_deinit(struct net2_signature *s)
 /* Fill s from an already computed digest (signature.n2t:74-100); shared
  * with the tick-batched carver step (signed_carver.c), hidden. */
 int
-sign_digest(struct net2_signature *s, const uint8_t *digest, size_t dlen,
-    const char *hash_name, struct net2_sign_ctx *sign)
+sign_digest(struct net2x_signature *s, const uint8_t *digest, size_t dlen,
+    const char *hash_name, struct net2x_sign_ctx *sign)
 {
-	size_t cap = net2_signctx_maxmsglen(sign);
+	size_t cap = net2x_signctx_maxmsglen(sign);
 	int rc;
 
 	memset(s, 0, sizeof(*s));
-	if ((s->sign_alg = dupstr(net2_signctx_name(sign))) == NULL ||
+	if ((s->sign_alg = dupstr(net2x_signctx_name(sign))) == NULL ||
 	    (s->hash_alg = dupstr(hash_name)) == NULL ||
 	    (s->data = malloc(cap ? cap : 1)) == NULL) {
-		net2_signature_deinit(s);
+		net2x_signature_deinit(s);
 		return ENOMEM;
 	}
 	s->datalen = cap;
-	if ((rc = net2_signctx_sign(sign, digest, dlen, s->data,
+	if ((rc = net2x_signctx_sign(sign, digest, dlen, s->data,
 	    &s->datalen)) != 0) {
-		net2_signature_deinit(s);
+		net2x_signature_deinit(s);
 		return rc;
 	}
 	return 0;
 }
 
 NET2_EXPORT int
-net2_signature_create(struct net2_signature *s, const struct iovec *to_sign,
-    size_t iovcnt, int hash_alg, struct net2_sign_ctx *sign)
+net2x_signature_create(struct net2x_signature *s, const struct iovec *to_sign,
+    size_t iovcnt, int hash_alg, struct net2x_sign_ctx *sign)
 {
 	const char *hash_name;
 	uint8_t digest[64];
@@ -93,7 +93,7 @@ net2_signature_create(struct net2_signature *s, const struct iovec *to_sign,
 
 /* signature.n2t:133-141 argument checks; returns the hash row or -errno. */
 static int
-validate_prologue(const struct net2_signature *s, int *valid)
+validate_prologue(const struct net2x_signature *s, int *valid)
 {
 	int alg;
 
@@ -111,8 +111,8 @@ validate_prologue(const struct net2_signature *s, int *valid)
 }
 
 NET2_EXPORT int
-net2_signature_validate(const struct net2_signature *s,
-    const struct iovec *to_sign, size_t iovcnt, struct net2_sign_ctx *sign,
+net2x_signature_validate(const struct net2x_signature *s,
+    const struct iovec *to_sign, size_t iovcnt, struct net2x_sign_ctx *sign,
     int *valid)
 {
 	uint8_t digest[64];
@@ -125,9 +125,9 @@ net2_signature_validate(const struct net2_signature *s,
 	if ((rc = net2_hashctx_hashiov(alg, NULL, 0, to_sign, iovcnt, digest,
 	    sizeof(digest))) != 0)
 		return ENOMEM;				/* signature.n2t:148-151 */
-	if (strcmp(net2_signctx_name(sign), s->sign_alg) != 0)
+	if (strcmp(net2x_signctx_name(sign), s->sign_alg) != 0)
 		return EINVAL;				/* signature.n2t:155-158 */
-	*valid = net2_signctx_validate(sign, s->data, s->datalen, digest,
+	*valid = net2x_signctx_validate(sign, s->data, s->datalen, digest,
 	    (size_t)net2_hash_gethashlen(alg));
 	return 0;
 }
@@ -140,9 +140,9 @@ struct ecdsa_job {
 	const uint8_t		*digests;
 	size_t			 dlen;
 	const char		*hash_name;
-	struct net2_sign_ctx	*sign;
-	struct net2_signature	*out;		/* create */
-	const struct net2_signature *sigs;	/* validate */
+	struct net2x_sign_ctx	*sign;
+	struct net2x_signature	*out;		/* create */
+	const struct net2x_signature *sigs;	/* validate */
 	const int		*alg_of;	/* validate: hash row or -errno */
 	const size_t		*dig_at;	/* validate: digest offset */
 	int			*valid;
@@ -161,9 +161,9 @@ ecdsa_worker(void *arg)
 			continue;
 		}
 		if (j->alg_of[i] < 0 ||
-		    strcmp(net2_signctx_name(j->sign), j->sigs[i].sign_alg) != 0)
+		    strcmp(net2x_signctx_name(j->sign), j->sigs[i].sign_alg) != 0)
 			continue;	/* valid[i] stays 0 */
-		j->valid[i] = net2_signctx_validate(j->sign, j->sigs[i].data,
+		j->valid[i] = net2x_signctx_validate(j->sign, j->sigs[i].data,
 		    j->sigs[i].datalen, j->digests + j->dig_at[i],
 		    (size_t)net2_hash_gethashlen(j->alg_of[i]));
 	}
@@ -206,9 +206,9 @@ run_ecdsa(struct ecdsa_job *proto, size_t n, int nthreads)
 }
 
 NET2_EXPORT int
-net2_signature_create_batch(struct net2_signature *out, const uint8_t *base,
+net2x_signature_create_batch(struct net2x_signature *out, const uint8_t *base,
     const uint64_t *offsets, const uint32_t *lens, size_t n, int hash_alg,
-    struct net2_sign_ctx *sign, int nthreads)
+    struct net2x_sign_ctx *sign, int nthreads)
 {
 	struct ecdsa_job job;
 	const char *hash_name;
@@ -240,16 +240,16 @@ net2_signature_create_batch(struct net2_signature *out, const uint8_t *base,
 		rc = run_ecdsa(&job, n, nthreads);
 		if (rc != 0)
 			for (size_t i = 0; i < n; i++)
-				net2_signature_deinit(&out[i]);
+				net2x_signature_deinit(&out[i]);
 	}
 	free(digests);
 	return rc;
 }
 
 NET2_EXPORT int
-net2_signature_validate_batch(const struct net2_signature *sigs,
+net2x_signature_validate_batch(const struct net2x_signature *sigs,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
-    size_t n, struct net2_sign_ctx *sign, int *valid, int nthreads)
+    size_t n, struct net2x_sign_ctx *sign, int *valid, int nthreads)
 {
 	struct ecdsa_job job;
 	int *alg_of = NULL;

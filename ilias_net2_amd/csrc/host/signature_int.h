@@ -8,7 +8,7 @@
 
 /* Fill s with the signature of an already computed digest
  * (types/signature.n2t:74-100); 0 or an errno, s left empty on failure. */
-int sign_digest(struct net2_signature *s, const uint8_t *digest, size_t dlen,
-    const char *hash_name, struct net2_sign_ctx *sign);
+int sign_digest(struct net2x_signature *s, const uint8_t *digest, size_t dlen,
+    const char *hash_name, struct net2x_sign_ctx *sign);
 
 #endif /* NET2_SIGNATURE_INT_H */

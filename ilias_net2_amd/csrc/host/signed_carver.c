@@ -2,12 +2,14 @@
  * signed_carver.c -- the hashing and signing steps of src/signed_carver.c,
  * batched per workq tick (include/net2/signed_carver.h).
  *
- * One tick: (1) every payload of the tick, from new carvers and from
- * combiner checks alike, is hashed once -- all payloads of one hash
- * algorithm in one net2_sha2_batch call (the reference hashes each payload
- * once per sign context, src/signed_carver.c:407-411 -> signature.n2t:92);
- * (2) the ECDSA work -- num_signatures signatures per carver (:407-432),
- * one verification per check (:305-319) -- is spread over host threads.
+ * One tick: (1) every payload of the tick, from hash requests, new
+ * carvers and combiner checks alike, is hashed once -- all payloads of one
+ * hash algorithm in one net2_sha2_batch call (the reference hashes each
+ * payload once per sign context, src/signed_carver.c:407-411 ->
+ * signature.n2t:92); (2) the work after the hash -- the hash requests'
+ * callbacks (the caller's own ECDSA, e.g. the reference's sign.c),
+ * num_signatures signatures per carver (:407-432), one verification per
+ * check (:305-319) -- is spread over host threads.
  */
 #include "../../../include/net2/signed_carver.h"
 #include "../../../include/net2/hash.h"
@@ -128,8 +130,11 @@ out:
 	return rc;
 }
 
-/* ECDSA jobs: job j < nsig_jobs signs, the rest validate. */
+/* Jobs after the hash: job j < nsig_jobs signs, the next nv validate, the
+ * last nh run the hash requests' callbacks. */
 struct ecdsa_plan {
+	struct net2_sc_hash_req		**hreq;
+	size_t				 nh;
 	struct net2_sc_sign_req		*sreq;
 	size_t				 ns;
 	struct net2_sc_validate_req	*vreq;
@@ -183,15 +188,22 @@ ecdsa_run(void *arg)
 				__atomic_store_n(&q->rc, rc, __ATOMIC_RELAXED);
 			continue;
 		}
+		if (j >= pl->nsig_jobs + pl->nv) {
+			struct net2_sc_hash_req *h =
+			    pl->hreq[j - pl->nsig_jobs - pl->nv];
+			if (h->done != NULL)
+				h->done(h, h->arg);
+			continue;
+		}
 		const size_t v = j - pl->nsig_jobs;
 		struct net2_sc_validate_req *q = &pl->vreq[v];
 		if (pl->valg[v] < 0 || q->result != 0)
 			continue;
-		if (strcmp(net2_signctx_name(q->sctx), q->sig->sign_alg) != 0) {
+		if (strcmp(net2x_signctx_name(q->sctx), q->sig->sign_alg) != 0) {
 			q->result = EIO;	/* signature.n2t:155-158 -> :333-336 */
 			continue;
 		}
-		q->result = net2_signctx_validate(q->sctx, q->sig->data,
+		q->result = net2x_signctx_validate(q->sctx, q->sig->data,
 		    q->sig->datalen, pl->vdig + 64 * v,
 		    (size_t)net2_hash_gethashlen(pl->valg[v])) == 1 ? 0 : EINVAL;
 	}
@@ -246,8 +258,19 @@ check_alg(const struct net2_sc_validate_req *q)
 	return alg;
 }
 
+/* a hash request's row: an unkeyed registry row with a digest */
 static int
-tick(struct net2_sc_sign_req *sreq, size_t ns,
+hash_req_ok(const struct net2_sc_hash_req *h)
+{
+	return !(h->payload == NULL && h->iovcnt > 0) &&
+	    net2_hash_getname(h->hash_alg) != NULL &&
+	    net2_hash_gethashlen(h->hash_alg) > 0 &&
+	    net2_hash_getkeylen(h->hash_alg) == 0;
+}
+
+static int
+tick(struct net2_sc_hash_req **hreq, size_t nh,
+    struct net2_sc_sign_req *sreq, size_t ns,
     struct net2_sc_validate_req *vreq, size_t nv, int nthreads)
 {
 	struct payload_ref *p = NULL;
@@ -256,9 +279,13 @@ tick(struct net2_sc_sign_req *sreq, size_t ns,
 	size_t *sjob = NULL, np = 0;
 	struct ecdsa_plan pl;
 
-	if (ns + nv == 0)
+	if (nh + ns + nv == 0)
 		return 0;
-	p = calloc(ns + nv, sizeof(*p));
+	for (size_t i = 0; i < nh; i++) {
+		hreq[i]->rc = hash_req_ok(hreq[i]) ? 0 : EINVAL;
+		hreq[i]->digestlen = 0;
+	}
+	p = calloc(nh + ns + nv, sizeof(*p));
 	sdig = malloc(ns * 64 + 1);
 	vdig = malloc(nv * 64 + 1);
 	valg = malloc((nv + 1) * sizeof(*valg));
@@ -270,9 +297,20 @@ tick(struct net2_sc_sign_req *sreq, size_t ns,
 			sreq[i].rc = ENOMEM;
 		for (size_t i = 0; i < nv; i++)
 			vreq[i].result = EIO;
+		/* every callback runs once, whatever the outcome */
+		for (size_t i = 0; i < nh; i++) {
+			hreq[i]->rc = ENOMEM;
+			if (hreq[i]->done != NULL)
+				hreq[i]->done(hreq[i], hreq[i]->arg);
+		}
 		goto out;
 	}
 	/* requests -> payloads to hash */
+	for (size_t i = 0; i < nh; i++) {
+		struct net2_sc_hash_req *h = hreq[i];
+		p[np++] = (struct payload_ref){ h->payload, h->iovcnt,
+		    h->rc == 0 ? h->hash_alg : -1, h->digest, &h->rc };
+	}
 	sjob[0] = 0;
 	for (size_t i = 0; i < ns; i++) {
 		struct net2_sc_sign_req *q = &sreq[i];
@@ -305,7 +343,13 @@ tick(struct net2_sc_sign_req *sreq, size_t ns,
 			vreq[i].result = EIO;	/* hash failure: :333-336 */
 			valg[i] = -1;
 		}
-	/* the ECDSA work on host threads */
+	for (size_t i = 0; i < nh; i++)
+		if (hreq[i]->rc == 0)
+			hreq[i]->digestlen =
+			    (uint32_t)net2_hash_gethashlen(hreq[i]->hash_alg);
+	/* the callbacks and the ECDSA work on host threads */
+	pl.hreq = hreq;
+	pl.nh = nh;
 	pl.sreq = sreq;
 	pl.ns = ns;
 	pl.vreq = vreq;
@@ -315,7 +359,7 @@ tick(struct net2_sc_sign_req *sreq, size_t ns,
 	pl.valg = valg;
 	pl.sjob = sjob;
 	pl.nsig_jobs = sjob[ns];
-	pl.njobs = sjob[ns] + nv;
+	pl.njobs = sjob[ns] + nv + nh;
 	if (pl.njobs > 0)
 		run_jobs(&pl, nthreads);
 	/* a carver whose signing failed keeps none of its signatures */
@@ -323,14 +367,18 @@ tick(struct net2_sc_sign_req *sreq, size_t ns,
 		if (sreq[i].rc != 0 && sreq[i].out != NULL &&
 		    sreq[i].rc != EINVAL)
 			for (uint32_t k = 0; k < sreq[i].num_signatures; k++)
-				net2_signature_deinit(&sreq[i].out[k]);
+				net2x_signature_deinit(&sreq[i].out[k]);
 	/* the tick failed as a whole only if every request did (a validation
 	 * that ran and found the signature invalid, EINVAL, is an outcome, not
 	 * a failure); then it returns the first request's error, which every
 	 * request carries too.  Otherwise 0, and the per-request rc / result
 	 * values are the outcome. */
-	if (ns + nv > 0) {
+	{
 		int all = 1, first = 0;
+		for (size_t i = 0; i < nh && all; i++) {
+			all = hreq[i]->rc != 0;
+			first = first ? first : hreq[i]->rc;
+		}
 		for (size_t i = 0; i < ns && all; i++) {
 			all = sreq[i].rc != 0;
 			first = first ? first : sreq[i].rc;
@@ -352,12 +400,38 @@ out:
 }
 
 NET2_EXPORT int
+net2_sc_hash_tick(struct net2_sc_hash_req *reqs, size_t n, int nthreads)
+{
+	struct net2_sc_hash_req **hp;
+	int rc;
+
+	if (n > 0 && reqs == NULL)
+		return EINVAL;
+	if (n == 0)
+		return 0;
+	if ((hp = malloc(n * sizeof(*hp))) == NULL) {
+		for (size_t i = 0; i < n; i++) {
+			reqs[i].rc = ENOMEM;
+			reqs[i].digestlen = 0;
+			if (reqs[i].done != NULL)
+				reqs[i].done(&reqs[i], reqs[i].arg);
+		}
+		return ENOMEM;
+	}
+	for (size_t i = 0; i < n; i++)
+		hp[i] = &reqs[i];
+	rc = tick(hp, n, NULL, 0, NULL, 0, nthreads);
+	free(hp);
+	return rc;
+}
+
+NET2_EXPORT int
 net2_signed_carver_sign_tick(struct net2_sc_sign_req *reqs, size_t n,
     int nthreads)
 {
 	if (n > 0 && reqs == NULL)
 		return EINVAL;
-	return tick(reqs, n, NULL, 0, nthreads);
+	return tick(NULL, 0, reqs, n, NULL, 0, nthreads);
 }
 
 NET2_EXPORT int
@@ -366,7 +440,7 @@ net2_signed_combiner_validate_tick(struct net2_sc_validate_req *reqs,
 {
 	if (n > 0 && reqs == NULL)
 		return EINVAL;
-	return tick(NULL, 0, reqs, n, nthreads);
+	return tick(NULL, 0, NULL, 0, reqs, n, nthreads);
 }
 
 /* ---- the collector ---------------------------------------------------- */
@@ -374,6 +448,8 @@ net2_signed_combiner_validate_tick(struct net2_sc_validate_req *reqs,
 struct net2_sc_collector {
 	pthread_mutex_t			 mu;
 	int				 nthreads;
+	struct net2_sc_hash_req		**hash;
+	size_t				 nhash, caphash;
 	struct net2_sc_sign_req		**sign;
 	size_t				 nsign, capsign;
 	struct net2_sc_validate_req	**val;
@@ -401,6 +477,7 @@ net2_sc_collector_free(struct net2_sc_collector *c)
 	if (c == NULL)
 		return;
 	pthread_mutex_destroy(&c->mu);
+	free(c->hash);
 	free(c->sign);
 	free(c->val);
 	free(c);
@@ -419,6 +496,20 @@ push(void ***arr, size_t *n, size_t *cap, void *item)
 	}
 	(*arr)[(*n)++] = item;
 	return 0;
+}
+
+NET2_EXPORT int
+net2_sc_collector_add_hash(struct net2_sc_collector *c,
+    struct net2_sc_hash_req *r)
+{
+	int rc;
+
+	if (c == NULL || r == NULL)
+		return EINVAL;
+	pthread_mutex_lock(&c->mu);
+	rc = push((void ***)&c->hash, &c->nhash, &c->caphash, r);
+	pthread_mutex_unlock(&c->mu);
+	return rc;
 }
 
 NET2_EXPORT int
@@ -450,18 +541,23 @@ net2_sc_collector_add_validate(struct net2_sc_collector *c,
 }
 
 NET2_EXPORT int
-net2_sc_collector_tick(struct net2_sc_collector *c, size_t *nsign,
-    size_t *nvalidate)
+net2_sc_collector_tick(struct net2_sc_collector *c, size_t *nhash,
+    size_t *nsign, size_t *nvalidate)
 {
+	struct net2_sc_hash_req **hp;
 	struct net2_sc_sign_req **sp, *sreq = NULL;
 	struct net2_sc_validate_req **vp, *vreq = NULL;
-	size_t ns, nv;
+	size_t nh, ns, nv;
 	int rc;
 
 	if (c == NULL)
 		return EINVAL;
 	/* take the tick's requests; later adds go to the next tick */
 	pthread_mutex_lock(&c->mu);
+	hp = c->hash;
+	nh = c->nhash;
+	c->hash = NULL;
+	c->nhash = c->caphash = 0;
 	sp = c->sign;
 	ns = c->nsign;
 	vp = c->val;
@@ -471,6 +567,8 @@ net2_sc_collector_tick(struct net2_sc_collector *c, size_t *nsign,
 	c->val = NULL;
 	c->nval = c->capval = 0;
 	pthread_mutex_unlock(&c->mu);
+	if (nhash != NULL)
+		*nhash = nh;
 	if (nsign != NULL)
 		*nsign = ns;
 	if (nvalidate != NULL)
@@ -483,6 +581,12 @@ net2_sc_collector_tick(struct net2_sc_collector *c, size_t *nsign,
 			sp[i]->rc = ENOMEM;
 		for (size_t i = 0; i < nv; i++)
 			vp[i]->result = EIO;
+		for (size_t i = 0; i < nh; i++) {
+			hp[i]->rc = ENOMEM;
+			hp[i]->digestlen = 0;
+			if (hp[i]->done != NULL)
+				hp[i]->done(hp[i], hp[i]->arg);
+		}
 		rc = ENOMEM;
 		goto out;
 	}
@@ -490,7 +594,7 @@ net2_sc_collector_tick(struct net2_sc_collector *c, size_t *nsign,
 		sreq[i] = *sp[i];
 	for (size_t i = 0; i < nv; i++)
 		vreq[i] = *vp[i];
-	rc = tick(sreq, ns, vreq, nv, c->nthreads);
+	rc = tick(hp, nh, sreq, ns, vreq, nv, c->nthreads);
 	for (size_t i = 0; i < ns; i++)
 		sp[i]->rc = sreq[i].rc;
 	for (size_t i = 0; i < nv; i++)
@@ -498,6 +602,7 @@ net2_sc_collector_tick(struct net2_sc_collector *c, size_t *nsign,
 out:
 	free(sreq);
 	free(vreq);
+	free(hp);
 	free(sp);
 	free(vp);
 	return rc;

@@ -1,5 +1,5 @@
 /*
- * wire.c -- encodings of net2_signature and signed_carver_header
+ * wire.c -- encodings of net2x_signature and signed_carver_header
  * (include/net2/wire.h has the layout and its reference citations).
  */
 #include "../../../include/net2/wire.h"
@@ -71,7 +71,7 @@ get_field(const uint8_t *p, size_t avail, const uint8_t **data,
 }
 
 NET2_EXPORT size_t
-net2_signature_encoded_len(const struct net2_signature *s)
+net2x_signature_encoded_len(const struct net2x_signature *s)
 {
 	if (s == NULL || s->sign_alg == NULL || s->hash_alg == NULL)
 		return 0;
@@ -80,10 +80,10 @@ net2_signature_encoded_len(const struct net2_signature *s)
 }
 
 NET2_EXPORT int
-net2_signature_encode(const struct net2_signature *s, void *out,
+net2x_signature_encode(const struct net2x_signature *s, void *out,
     size_t *outlen)
 {
-	size_t need = net2_signature_encoded_len(s);
+	size_t need = net2x_signature_encoded_len(s);
 	uint8_t *p = out;
 
 	if (need == 0 || outlen == NULL || out == NULL || *outlen < need ||
@@ -111,7 +111,7 @@ strndup_field(const uint8_t *d, size_t l)
 }
 
 NET2_EXPORT int
-net2_signature_decode(struct net2_signature *s, const void *in,
+net2x_signature_decode(struct net2x_signature *s, const void *in,
     size_t inlen, size_t *consumed)
 {
 	const uint8_t *p = in, *d[3];
@@ -129,7 +129,7 @@ net2_signature_decode(struct net2_signature *s, const void *in,
 	s->hash_alg = strndup_field(d[1], l[1]);
 	s->data = malloc(l[2] ? l[2] : 1);
 	if (s->sign_alg == NULL || s->hash_alg == NULL || s->data == NULL) {
-		net2_signature_deinit(s);
+		net2x_signature_deinit(s);
 		return memchr(d[0], 0, l[0]) || memchr(d[1], 0, l[1]) ? EINVAL
 		    : ENOMEM;
 	}

@@ -1190,7 +1190,7 @@ NET2_EXPORT int net2_hmac_dev(int alg, const void *key, size_t keylen,
 	return 0;
 }
 
-NET2_EXPORT int net2_ph_to_iv(const struct net2_packet_header *ph,
+NET2_EXPORT int net2_ph_to_iv_buf(const struct net2_packet_header *ph,
     size_t ivlen, void *iv)
 {
 	uint8_t hdr[8];

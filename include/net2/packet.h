@@ -23,12 +23,14 @@ struct net2_packet_header {
 };
 
 /*
- * net2_ph_to_iv: iv = first ivlen bytes of the chain
+ * net2_ph_to_iv_buf: the reference's net2_ph_to_iv (a decoded header in,
+ * the IV into a plain buffer; the reference's own name and prototype stay
+ * the reference's, packet.n2t:100-158).  iv = first ivlen bytes of the chain
  * iv += SHA-256(ph_network || iv) (packet.n2t:127-144), any ivlen.
  * Synchronous, one header; the SHA-256s run on the GPU.
  * 0, EINVAL, ENOMEM, ENODEV or EIO.
  */
-int net2_ph_to_iv(const struct net2_packet_header *ph, size_t ivlen,
+int net2_ph_to_iv_buf(const struct net2_packet_header *ph, size_t ivlen,
     void *iv);
 
 /*

@@ -5,7 +5,7 @@
  * (src/signed_carver.c:385-466, :265-338) hash a whole batch of payloads in
  * one GPU launch.
  *
- * struct net2_signature mirrors the n2t type (signature.n2t:48-53):
+ * struct net2x_signature mirrors the n2t type (signature.n2t:48-53):
  * { string sign_alg; string hash_alg; short_net2_buffer data; }.
  */
 #ifndef NET2_SIGNATURE_H
@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-struct net2_signature {
+struct net2x_signature {
 	char		*sign_alg;	/* e.g. "ecdsa" */
 	char		*hash_alg;	/* registry name, e.g. "SHA512" */
 	uint8_t		*data;		/* DER signature of the digest */
@@ -33,21 +33,21 @@ struct net2_signature {
  * the GPU, sign the digest.  0, EINVAL (NULL argument / unknown alg),
  * ENOMEM, or the errno of the hash or sign step.
  */
-int net2_signature_create(struct net2_signature *s,
+int net2x_signature_create(struct net2x_signature *s,
     const struct iovec *to_sign, size_t iovcnt, int hash_alg,
-    struct net2_sign_ctx *sign);
+    struct net2x_sign_ctx *sign);
 
 /*
  * signature.n2t:124-175: *valid = 0 first; EINVAL for NULL arguments or a
  * mismatching sign algorithm, EOPNOTSUPP for an unknown hash name, else 0
  * with *valid = 1 iff the signature matches.
  */
-int net2_signature_validate(const struct net2_signature *s,
-    const struct iovec *to_sign, size_t iovcnt, struct net2_sign_ctx *sign,
+int net2x_signature_validate(const struct net2x_signature *s,
+    const struct iovec *to_sign, size_t iovcnt, struct net2x_sign_ctx *sign,
     int *valid);
 
 /* signature.n2t:177-189. */
-void net2_signature_deinit(struct net2_signature *s);
+void net2x_signature_deinit(struct net2x_signature *s);
 
 /*
  * Batched create: payload i = base[offsets[i] .. + lens[i]) in host memory.
@@ -56,18 +56,18 @@ void net2_signature_deinit(struct net2_signature *s);
  * most 64).  out[0 .. n) are initialised on success; on failure none are
  * left allocated.
  */
-int net2_signature_create_batch(struct net2_signature *out,
+int net2x_signature_create_batch(struct net2x_signature *out,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
-    size_t n, int hash_alg, struct net2_sign_ctx *sign, int nthreads);
+    size_t n, int hash_alg, struct net2x_sign_ctx *sign, int nthreads);
 
 /*
  * Batched validate of sigs[i] over payload i (same layout); valid[i] as in
- * net2_signature_validate.  Signatures may name different hash algorithms;
+ * net2x_signature_validate.  Signatures may name different hash algorithms;
  * each algorithm's payloads are hashed in one batch.
  */
-int net2_signature_validate_batch(const struct net2_signature *sigs,
+int net2x_signature_validate_batch(const struct net2x_signature *sigs,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
-    size_t n, struct net2_sign_ctx *sign, int *valid, int nthreads);
+    size_t n, struct net2x_sign_ctx *sign, int *valid, int nthreads);
 
 #ifdef __cplusplus
 }

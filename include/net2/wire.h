@@ -25,19 +25,19 @@
 extern "C" {
 #endif
 
-/* Bytes net2_signature_encode needs for s. */
-size_t net2_signature_encoded_len(const struct net2_signature *s);
+/* Bytes net2x_signature_encode needs for s. */
+size_t net2x_signature_encoded_len(const struct net2x_signature *s);
 
 /* Encode s into out (capacity *outlen; length written back). 0 / EINVAL. */
-int net2_signature_encode(const struct net2_signature *s, void *out,
+int net2x_signature_encode(const struct net2x_signature *s, void *out,
     size_t *outlen);
 
 /*
  * Decode one signature from in[0 .. inlen) into s (allocates; free with
- * net2_signature_deinit); *consumed = bytes used.  0, EINVAL (truncated or
+ * net2x_signature_deinit); *consumed = bytes used.  0, EINVAL (truncated or
  * non-zero padding), ENOMEM.
  */
-int net2_signature_decode(struct net2_signature *s, const void *in,
+int net2x_signature_decode(struct net2x_signature *s, const void *in,
     size_t inlen, size_t *consumed);
 
 struct net2_signed_carver_header {

@@ -245,7 +245,7 @@ def test_many_threads_mixed(L, oracle_mod):
                     seq, fl = int(rng.integers(0, 2**32)), int(rng.integers(0, 2**32))
                     ivlen = int(rng.integers(1, 80))
                     out = ctypes.create_string_buffer(ivlen)
-                    rc = L.net2_ph_to_iv(ctypes.byref(PH(seq, fl)), ivlen, out)
+                    rc = L.net2_ph_to_iv_buf(ctypes.byref(PH(seq, fl)), ivlen, out)
                     if rc != 0 or out.raw[:ivlen] != oracle_mod.ph_to_iv(seq, fl, ivlen):
                         errors.append(("iv", t, j, rc))
         except Exception as e:  # noqa: BLE001

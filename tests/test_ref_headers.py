@@ -183,3 +183,147 @@ def test_cxx_backend_against_reference_hash_h(tmp_path):
               os.path.join(ROOT, "ilias_net2_amd", "csrc", "cxx", "hash_mi355x.cc")])
     assert r.returncode == 0, r.stderr[-4000:]
     assert " error" not in r.stderr
+
+
+# --- the sign-layer boundary ----------------------
+
+# The reference's C net2_buffer API is declared nowhere in its tree (its
+# buffer.h is the C++ ilias::buffer); the INTEGRATION.md
+# snippets call five of its functions, declared here with the prototypes
+# their reference call sites imply.  net2_workq_cb is likewise used by the
+# reference's own signed_carver.h:77 and declared nowhere (the C workq API
+# became C++ workq.h); its shape is the (void*, void*) callback of
+# net2_signed_carver_set_rts.
+_LOST_C_API = r"""
+#include <errno.h>
+#include <string.h>
+#include <sys/uio.h>
+struct net2_buffer;
+extern "C" {
+typedef void (*net2_workq_cb)(void *, void *);
+struct net2_buffer *net2_buffer_new(void);                        /* signed_carver.c:415 */
+void   net2_buffer_free(struct net2_buffer *);                    /* signed_carver.c:424 */
+int    net2_buffer_add(struct net2_buffer *, const void *, size_t);  /* enc.c:307 */
+size_t net2_buffer_length(const struct net2_buffer *);            /* sign.c:524 */
+size_t net2_buffer_peek(const struct net2_buffer *, size_t,
+    struct iovec *, size_t);                                      /* sign.c:290,294 */
+int    net2_buffer_reserve_space(struct net2_buffer *, size_t,
+    struct iovec *, size_t *);                                    /* sign.c:283,502 */
+int    net2_buffer_commit_space(struct net2_buffer *, struct iovec *,
+    size_t);                                                      /* sign.c:308,512 */
+}
+"""
+
+
+def _integration_snippets():
+    """The ```c blocks of INTEGRATION.md marked as compiled."""
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    blocks = re.findall(
+        r"<!-- compiled: tests/test_ref_headers.py -->\s*```c\n(.*?)```",
+        text, flags=re.S)
+    return blocks
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
+def test_integration_carver_binding_compiles_with_reference_headers(tmp_path):
+    """One TU: the reference's own include/ilias/net2/sign.h and
+    signed_carver.h, this repository's include/net2/signed_carver.h (and
+    with it net2/sign.h, net2/signature.h) and net2/hash.h, and every
+    INTEGRATION.md block marked compiled (the hash registry's hashbuf and
+    the signed carver's tick binding).  g++ (the reference's headers are
+    C++): no error, so no conflicting declaration -- a C-linkage function
+    declared twice with different prototypes is an error in C++."""
+    blocks = _integration_snippets()
+    assert len(blocks) >= 2, "INTEGRATION.md lost its compiled blocks"
+    assert any("net2_sc_hash_req" in b for b in blocks)
+    cfg_inc, _ = _instantiate_config(str(tmp_path))
+    tu = os.path.join(str(tmp_path), "binding.cc")
+    with open(tu, "w") as fh:
+        fh.write(_LOST_C_API)
+        fh.write("#include <ilias/net2/sign.h>\n"
+                 "#include <ilias/net2/signed_carver.h>\n")
+        for b in blocks:
+            fh.write(b)
+            fh.write("\n")
+    r = _run(["g++", "-std=c++11", "-fsyntax-only", "-w", "-include", "limits",
+              "-I", cfg_inc, "-I", os.path.join(REF, "include"),
+              "-I", os.path.join(ROOT, "include"), tu])
+    assert r.returncode == 0, r.stderr[-4000:]
+    # the binding really uses the reference's own sign calls
+    body = "\n".join(blocks)
+    for name in ("net2_signctx_sign(", "net2_signctx_validate(",
+                 "net2_sc_collector_add_hash(", "net2_sc_collector_tick("):
+        assert name in body, name
+
+
+def _ref_declared_and_defined():
+    """Identifiers the reference declares in include/ (a name followed by
+    '(' in a prototype, or an extern object) or defines in its sources
+    (BSD style: the function name at the start of a line)."""
+    names = set()
+    for top in ("include", "src", "types", "cxx_src"):
+        for dp, _, fs in os.walk(os.path.join(REF, top)):
+            for f in fs:
+                if not f.endswith((".h", ".c", ".n2t", ".cc")):
+                    continue
+                txt = open(os.path.join(dp, f), errors="replace").read()
+                if top == "include":
+                    names |= set(re.findall(r"\b(net2_\w+|SHA\w+)\s*\(", txt))
+                    names |= set(re.findall(r"extern\s+[^;()]*?\b(net2_\w+)\s*;", txt))
+                names |= set(re.findall(r"^(net2_\w+|SHA\w+)\(", txt, flags=re.M))
+    return names
+
+
+# Reference names the shipped libraries may export, and why their
+# prototypes are the reference's:
+#  * SHA*: src/sha2.c defines them and compiles unchanged against
+#    include/net2/sha2.h, which declares them
+#    (test_reference_sha2_c_compiles_against_drop_in_header: a definition
+#    that disagreed with its declaration would not compile).
+#  * the C hash registry (net2_hash_*, net2_hashmax): declared and defined
+#    nowhere in the reference (its hash.c and header are lost, SURVEY.md
+#    8b B1); include/net2/hash.h restores them from their call sites.
+_REGISTRY = {"net2_hash_getname", "net2_hash_findname", "net2_hash_gethashlen",
+             "net2_hash_getkeylen", "net2_hashmax"}
+
+
+def test_no_shipped_library_exports_a_reference_name_with_another_prototype():
+    libs = [os.path.join(ROOT, "ilias_net2_amd", n) for n in
+            ("libnet2_sha2.so", "libnet2_sign.so", "libnet2_hash_cxx.so")]
+    libs = [l for l in libs if os.path.exists(l)]
+    if not libs:
+        pytest.skip("libraries not built")
+    exported = set()
+    for lib in libs:
+        r = _run(["nm", "-D", "--defined-only", lib])
+        assert r.returncode == 0, r.stderr
+        exported |= set(re.findall(r"^\S+ [TDRB] (\S+)$", r.stdout, flags=re.M))
+    ref = _ref_declared_and_defined()
+    assert "net2_signctx_sign" in ref and "SHA256Update" in ref  # sanity
+    clash = sorted(exported & ref)
+    sha = {s for s in clash if re.fullmatch(r"SHA(256|384|512)\w+", s)}
+    assert len(sha) == 15, sha
+    rest = set(clash) - sha
+    assert rest <= _REGISTRY, rest
+    # the registry really is declared / defined nowhere in the reference
+    inc = []
+    for dp, _, fs in os.walk(os.path.join(REF, "include")):
+        inc += [open(os.path.join(dp, f), errors="replace").read() for f in fs]
+    for name in _REGISTRY:
+        assert not any(re.search(r"\b%s\b" % name, t) for t in inc), name
+    # the reference's sign.h / signature.n2t / packet.n2t names in particular
+    for name in ("net2_signctx_sign", "net2_signctx_validate",
+                 "net2_signctx_pubkey", "net2_signctx_fingerprint",
+                 "net2_signctx_pubnew", "net2_signmax", "net2_sign_ecdsa",
+                 "net2_signature_create", "net2_signature_validate",
+                 "net2_signature_deinit", "net2_ph_to_iv",
+                 "net2_hashctx_hashbuf"):
+        assert name not in exported, name
+    # C++ exports: only the factories of the reference's hash.h:73-79,
+    # whose declarations the backend is type-checked against
+    # (test_cxx_backend_against_reference_hash_h)
+    cxx = {s for s in exported if s.startswith("_ZN5ilias")}
+    assert cxx == {"_ZN5ilias4hash6sha256Ev", "_ZN5ilias4hash6sha384Ev",
+                   "_ZN5ilias4hash6sha512Ev", "_ZN5ilias4hash11hmac_sha256Ev",
+                   "_ZN5ilias4hash11hmac_sha384Ev",
+                   "_ZN5ilias4hash11hmac_sha512Ev"}, cxx

@@ -1,4 +1,4 @@
-"""CPU: wire encodings of net2_signature (types/signature.n2t:48-53) and
+"""CPU: wire encodings of net2x_signature (types/signature.n2t:48-53) and
 signed_carver_header (types/signed_carver_header.n2t:21-43).
 
 The byte layout is restated independently here from the reference's
@@ -28,8 +28,8 @@ def _lib():
     import ilias_net2_amd._lib as L
     L.lib()
     lib = ctypes.CDLL(os.path.join(ROOT, "ilias_net2_amd", "libnet2_sign.so"))
-    lib.net2_signature_encoded_len.restype = ctypes.c_size_t
-    lib.net2_signature_deinit.restype = None
+    lib.net2x_signature_encoded_len.restype = ctypes.c_size_t
+    lib.net2x_signature_deinit.restype = None
     return lib
 
 
@@ -53,20 +53,20 @@ def test_signature_encode_matches_reference_layout():
             s = Sig(sa, ha, buf, n)
             want = ref_signature(sa, ha, data)
             assert len(want) % 8 == 0
-            assert lib.net2_signature_encoded_len(ctypes.byref(s)) == len(want)
+            assert lib.net2x_signature_encoded_len(ctypes.byref(s)) == len(want)
             out = ctypes.create_string_buffer(len(want))
             olen = ctypes.c_size_t(len(want))
-            assert lib.net2_signature_encode(ctypes.byref(s), out, ctypes.byref(olen)) == 0
+            assert lib.net2x_signature_encode(ctypes.byref(s), out, ctypes.byref(olen)) == 0
             assert out.raw[:olen.value] == want
             # decode round trip
             d = Sig()
             used = ctypes.c_size_t(0)
             enc = want + b"trailing"
-            assert lib.net2_signature_decode(ctypes.byref(d), enc, len(enc), ctypes.byref(used)) == 0
+            assert lib.net2x_signature_decode(ctypes.byref(d), enc, len(enc), ctypes.byref(used)) == 0
             assert used.value == len(want)
             assert (d.sign_alg or b"") == sa and (d.hash_alg or b"") == ha
             assert bytes(d.data[:d.datalen]) == data
-            lib.net2_signature_deinit(ctypes.byref(d))
+            lib.net2x_signature_deinit(ctypes.byref(d))
 
 
 def test_signature_decode_rejects_malformed():
@@ -75,13 +75,13 @@ def test_signature_decode_rejects_malformed():
     d = Sig()
     used = ctypes.c_size_t()
     for bad in (good[:-1], good[:3], b"", good[:9] + b"\x01" + good[10:]):
-        assert lib.net2_signature_decode(ctypes.byref(d), bad, len(bad), ctypes.byref(used)) == errno.EINVAL
+        assert lib.net2x_signature_decode(ctypes.byref(d), bad, len(bad), ctypes.byref(used)) == errno.EINVAL
     huge = struct.pack(">I", 0xFFFFFFF0) + b"\0" * 12
-    assert lib.net2_signature_decode(ctypes.byref(d), huge, len(huge), ctypes.byref(used)) == errno.EINVAL
+    assert lib.net2x_signature_decode(ctypes.byref(d), huge, len(huge), ctypes.byref(used)) == errno.EINVAL
     small = ctypes.c_size_t(3)
     s = Sig(b"ecdsa", b"SHA512", None, 0)
     out = ctypes.create_string_buffer(64)
-    assert lib.net2_signature_encode(ctypes.byref(s), out, ctypes.byref(small)) == errno.EINVAL
+    assert lib.net2x_signature_encode(ctypes.byref(s), out, ctypes.byref(small)) == errno.EINVAL
 
 
 def test_signed_carver_header():

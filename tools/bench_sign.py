@@ -5,7 +5,7 @@ payloads, hash-then-sign (types/signature.n2t:60-119) and validate
 
 Reports, per stage: the GPU batch digest (net2_sha2_batch, host memory in
 and out), ECDSA over the digests on host threads, and the batched
-net2_signature_create_batch / _validate_batch end to end; plus the same flow
+net2x_signature_create_batch / _validate_batch end to end; plus the same flow
 with the oracle's CPU digests (the reference's per-payload SHA512 on one
 core, test/sign.c's shape) as the baseline.  One JSON line per measurement.
 """
@@ -66,15 +66,15 @@ def stages():
     import synth
     L.lib()
     S = ctypes.CDLL(os.path.join(ROOT, "ilias_net2_amd", "libnet2_sign.so"))
-    S.net2_signctx_privnew.restype = ctypes.c_void_p
-    S.net2_signctx_pubnew.restype = ctypes.c_void_p
-    S.net2_signctx_maxmsglen.restype = ctypes.c_size_t
-    S.net2_signctx_maxmsglen.argtypes = [ctypes.c_void_p]
-    S.net2_signature_deinit.restype = None
+    S.net2x_signctx_privnew.restype = ctypes.c_void_p
+    S.net2x_signctx_pubnew.restype = ctypes.c_void_p
+    S.net2x_signctx_maxmsglen.restype = ctypes.c_size_t
+    S.net2x_signctx_maxmsglen.argtypes = [ctypes.c_void_p]
+    S.net2x_signature_deinit.restype = None
     keys = [open(os.path.join(ROOT, "tests", "golden", "keys", f), "rb").read()
             for f in ("ecdsa_p521_priv.pem", "ecdsa_p521_pub.pem")]
-    priv = ctypes.c_void_p(S.net2_signctx_privnew(0, keys[0], len(keys[0])))
-    pub = ctypes.c_void_p(S.net2_signctx_pubnew(0, keys[1], len(keys[1])))
+    priv = ctypes.c_void_p(S.net2x_signctx_privnew(0, keys[0], len(keys[0])))
+    pub = ctypes.c_void_p(S.net2x_signctx_pubnew(0, keys[1], len(keys[1])))
     assert priv and pub
     n, length = 4096, 1024
     threads = min(16, len(os.sched_getaffinity(0)))
@@ -109,18 +109,18 @@ def stages():
     valid = (ctypes.c_int * n)()
 
     def create():
-        rc = S.net2_signature_create_batch(sigs, ptr(data), ptr(offs), ptr(lens),
+        rc = S.net2x_signature_create_batch(sigs, ptr(data), ptr(offs), ptr(lens),
                                            ctypes.c_size_t(n), 3, priv, threads)
         assert rc == 0, rc
 
     def validate():
-        rc = S.net2_signature_validate_batch(sigs, ptr(data), ptr(offs), ptr(lens),
+        rc = S.net2x_signature_validate_batch(sigs, ptr(data), ptr(offs), ptr(lens),
                                              ctypes.c_size_t(n), pub, valid, threads)
         assert rc == 0, rc
 
     def free_all():
         for i in range(n):
-            S.net2_signature_deinit(ctypes.byref(sigs[i]))
+            S.net2x_signature_deinit(ctypes.byref(sigs[i]))
 
     create()
     t_c = 1e9
@@ -132,10 +132,10 @@ def stages():
     t_v = timeit(validate, reps=2)
     assert all(v == 1 for v in valid)
     res.append({"key": "signature_create_batch",
-                "stage": f"net2_signature_create_batch SHA512+ECDSA-P521, {threads} threads",
+                "stage": f"net2x_signature_create_batch SHA512+ECDSA-P521, {threads} threads",
                 "payloads_per_s": n / t_c, "ms": t_c * 1e3})
     res.append({"key": "signature_validate_batch",
-                "stage": f"net2_signature_validate_batch SHA512+ECDSA-P521, {threads} threads",
+                "stage": f"net2x_signature_validate_batch SHA512+ECDSA-P521, {threads} threads",
                 "payloads_per_s": n / t_v, "ms": t_v * 1e3})
     free_all()
 
@@ -164,7 +164,7 @@ def stages():
 
     def sign_tick():
         for i in range(n):
-            S.net2_signature_deinit(ctypes.byref(outs[i]))
+            S.net2x_signature_deinit(ctypes.byref(outs[i]))
         rc = S.net2_signed_carver_sign_tick(reqs, ctypes.c_size_t(n), threads)
         assert rc == 0, rc
 
@@ -182,7 +182,7 @@ def stages():
                 "stage": f"net2_signed_combiner_validate_tick: {n} checks, one tick, {threads} threads",
                 "payloads_per_s": n / t_vt, "ms": t_vt * 1e3})
     for i in range(n):
-        S.net2_signature_deinit(ctypes.byref(outs[i]))
+        S.net2x_signature_deinit(ctypes.byref(outs[i]))
     return res
 
 
