@@ -52,6 +52,17 @@ def lib() -> ctypes.CDLL:
         L.oracle_sha2_batch_ex.restype = ctypes.c_int
         L.oracle_ph_to_iv.argtypes = [ctypes.c_uint32, ctypes.c_uint32, sz, vp]
         L.oracle_ph_to_iv.restype = ctypes.c_int
+        u32, u64, i = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+        L.oracle_hmac_batch.argtypes = [i, vp, sz, vp, vp, vp, u64, u32, sz, vp, i]
+        L.oracle_ph_to_iv_batch.argtypes = [vp, vp, sz, sz, vp, i]
+        L.oracle_packet_decode_batch.argtypes = [i, vp, sz, vp, sz, i, u32, u32,
+                                                 i, sz, vp, vp, vp, sz, vp, vp,
+                                                 vp, vp, i]
+        L.oracle_packet_encode_batch.argtypes = [i, vp, sz, i, vp, vp, vp, vp, vp,
+                                                 sz, vp, i]
+        for f in ("oracle_hmac_batch", "oracle_ph_to_iv_batch",
+                  "oracle_packet_decode_batch", "oracle_packet_encode_batch"):
+            getattr(L, f).restype = ctypes.c_int
         for pfx in ("sha256", "sha384", "sha512"):
             for fn, args in (("init", [vp]), ("update", [vp, vp, sz]),
                              ("pad", [vp]), ("final", [vp, vp])):
@@ -138,3 +149,85 @@ def ph_to_iv(seq: int, flags: int, ivlen: int) -> bytes:
     out = ctypes.create_string_buffer(max(ivlen, 1))
     lib().oracle_ph_to_iv(seq, flags, ivlen, out)
     return out.raw[:ivlen]
+
+
+def _nthreads(nthreads):
+    return nthreads if nthreads else min(16, os.cpu_count() or 1)
+
+
+def _keybuf(key):
+    return None if key is None else ctypes.create_string_buffer(bytes(key), max(len(key), 1))
+
+
+def hmac_batch(alg: int, key: bytes, data: np.ndarray, offsets=None, lens=None,
+               stride=0, length=0, n=None, nthreads=0) -> np.ndarray:
+    """HMAC (alg 4..6) of every packet under one key, threaded; layouts as
+    batch()."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    if offsets is not None:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        n = len(offsets)
+    out = np.empty((n, DIGEST_LEN[alg]), dtype=np.uint8)
+    kb = _keybuf(key)
+    if lib().oracle_hmac_batch(alg, kb, len(key), _ptr(data), _ptr(offsets),
+                               _ptr(lens), stride, length, n, _ptr(out),
+                               _nthreads(nthreads)) != 0:
+        raise ValueError(f"bad alg {alg}")
+    return out
+
+
+def ph_to_iv_batch(seq: np.ndarray, flags: np.ndarray, ivlen: int,
+                   nthreads=0) -> np.ndarray:
+    seq = np.ascontiguousarray(seq, dtype=np.uint32)
+    flags = np.ascontiguousarray(flags, dtype=np.uint32)
+    out = np.zeros((len(seq), max(ivlen, 1)), dtype=np.uint8)
+    lib().oracle_ph_to_iv_batch(_ptr(seq), _ptr(flags), len(seq), ivlen,
+                                _ptr(out), _nthreads(nthreads))
+    return out[:, :ivlen]
+
+
+def packet_decode_batch(hash_alg: int, key: bytes, enc_set: bool, ivlen: int,
+                        data: np.ndarray, offsets, lens, alt_key=None,
+                        alt_no_cutoff=False, alt_cutoff=0, rx_start=0,
+                        nthreads=0):
+    """The hash steps of net2_packet_decode over a burst (see
+    oracle_packet_decode_batch): (result u8[n], iv u8[n, ivlen],
+    seq u32[n], flags u32[n]); iv rows with no IV due are zero."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    n = len(offsets)
+    res = np.full(n, 9, dtype=np.uint8)
+    iv = np.zeros((n, max(ivlen, 1)), dtype=np.uint8)
+    seq = np.zeros(n, dtype=np.uint32)
+    fl = np.zeros(n, dtype=np.uint32)
+    key = key or b""
+    if lib().oracle_packet_decode_batch(
+            hash_alg, _keybuf(key), len(key), _keybuf(alt_key),
+            len(alt_key) if alt_key is not None else 0, int(alt_no_cutoff),
+            alt_cutoff, rx_start, int(enc_set), ivlen, _ptr(data), _ptr(offsets),
+            _ptr(lens), n, _ptr(res), _ptr(iv) if ivlen else None, _ptr(seq),
+            _ptr(fl), _nthreads(nthreads)) != 0:
+        raise ValueError(f"bad alg {hash_alg}")
+    return res, iv[:, :ivlen], seq, fl
+
+
+def packet_encode_batch(hash_alg: int, key: bytes, enc_set: bool, seq, flags,
+                        data: np.ndarray, offsets, lens, nthreads=0):
+    """The hash steps of net2_packet_encode over a burst, on a copy of data:
+    (result u8[n], sealed bytes)."""
+    out = np.array(data, dtype=np.uint8, copy=True)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    seq = np.ascontiguousarray(seq, dtype=np.uint32)
+    flags = np.ascontiguousarray(flags, dtype=np.uint32)
+    n = len(offsets)
+    res = np.full(n, 9, dtype=np.uint8)
+    key = key or b""
+    if lib().oracle_packet_encode_batch(
+            hash_alg, _keybuf(key), len(key), int(enc_set), _ptr(seq), _ptr(flags),
+            _ptr(out), _ptr(offsets), _ptr(lens), n, _ptr(res),
+            _nthreads(nthreads)) != 0:
+        raise ValueError(f"bad alg {hash_alg}")
+    return res, out

@@ -107,4 +107,30 @@ int oracle_ph_to_iv(uint32_t seq, uint32_t flags, size_t ivlen, uint8_t *iv);
 #ifdef __cplusplus
 }
 #endif
+/*
+ * Threaded batch forms (each item independent), so full-size GPU tests
+ * check every result against the oracle.  HMAC over a batch under one key
+ * (alg 4..6, layouts as oracle_sha2_batch); ph_to_iv of n headers into
+ * iv + i * ivlen; the hash steps of net2_packet_decode / _encode
+ * (types/packet.n2t:170-336 / :341-463) over a burst, as
+ * net2_packet_decode_burst_ck / net2_packet_encode_burst define it
+ * (alt_key NULL: no alternate rx key).  0, or -1 for a bad alg.
+ */
+int oracle_hmac_batch(int alg, const uint8_t *key, size_t keylen,
+    const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
+    uint64_t stride, uint32_t fixed_len, size_t n, uint8_t *out,
+    int nthreads);
+int oracle_ph_to_iv_batch(const uint32_t *seq, const uint32_t *flags,
+    size_t n, size_t ivlen, uint8_t *iv, int nthreads);
+int oracle_packet_decode_batch(int hash_alg, const uint8_t *key,
+    size_t keylen, const uint8_t *alt_key, size_t alt_keylen,
+    int alt_no_cutoff, uint32_t alt_cutoff, uint32_t rx_start, int enc_set,
+    size_t ivlen, const uint8_t *base, const uint64_t *offsets,
+    const uint32_t *lens, size_t n, uint8_t *result, uint8_t *iv,
+    uint32_t *seq_out, uint32_t *flags_out, int nthreads);
+int oracle_packet_encode_batch(int hash_alg, const uint8_t *key,
+    size_t keylen, int enc_set, const uint32_t *seq, const uint32_t *flags,
+    uint8_t *base, const uint64_t *offsets, const uint32_t *lens, size_t n,
+    uint8_t *result, int nthreads);
+
 #endif /* NET2_SHA2_ORACLE_H */

@@ -11,6 +11,7 @@ neither).
 """
 import ctypes
 import errno
+import os
 import struct
 
 import numpy as np
@@ -25,6 +26,7 @@ torch = pytest.importorskip("torch")
 PH_ENCRYPTED, PH_SIGNED, PH_ALTKEY = 0x1, 0x2, 0x80000000
 OK, RESOURCE, BAD, UNSAFE = 0, 1, 2, 3
 HL = {0: 0, 4: 32, 5: 48, 6: 64}
+CPU_THREADS = min(16, len(os.sched_getaffinity(0)))
 
 
 @pytest.fixture(scope="module")
@@ -279,11 +281,13 @@ def test_decode_burst_alternate_key(dev, oracle_mod, hash_alg, no_cutoff):
 
 def test_burst_round_trip_full_size(dev, oracle_mod):
     """The burst bench config at full size (1 M wire datagrams of {136, 584,
-    1500} B, HMAC-SHA512, 16-byte IVs), through properties that do not
-    depend on the size: encode then decode accepts every datagram; each IV
-    equals the device batch net2_ph_to_iv_dev gives for the decoded header;
-    sampled hash fields and IVs equal the oracle's; flipping one payload byte
-    in a chosen set of datagrams makes exactly those NET2_PDECODE_BAD."""
+    1500} B, HMAC-SHA512, 16-byte IVs), every result against the oracle's
+    restatement of the packet.n2t hash steps (oracle_packet_encode_batch /
+    _decode_batch): the sealed bytes and codes of every slot, then the
+    decode codes, headers and IVs of every datagram, intact and with one
+    payload byte flipped in a chosen set.  Kept beside them, the
+    size-independent properties: encode then decode accepts everything, the
+    IVs equal net2_ph_to_iv_dev's, exactly the tampered datagrams fail."""
     from ilias_net2_amd import _lib
     L = _lib.lib()
     n, hl, ivlen, alg = 1 << 20, 64, 16, 6
@@ -300,6 +304,12 @@ def test_burst_round_trip_full_size(dev, oracle_mod):
                         generator=g)
     flags = torch.full((n,), PH_SIGNED | PH_ENCRYPTED, dtype=torch.int32, device=dev)
     key = bytes(range(7, 7 + hl))
+    offs_h, lens_h = offs.cpu().numpy(), lens.cpu().numpy()
+    seq_h = seq.cpu().numpy().view(np.uint32)
+    fl_h = flags.cpu().numpy().view(np.uint32)
+    o_res, o_sealed = oracle_mod.packet_encode_batch(
+        alg, key, True, seq_h, fl_h, data.cpu().numpy(), offs_h, lens_h,
+        nthreads=CPU_THREADS)
     res = torch.full((n,), 9, dtype=torch.uint8, device=dev)
     ws = torch.empty(L.net2_packet_burst_workspace(n), dtype=torch.uint8, device=dev)
     st = torch.cuda.current_stream().cuda_stream
@@ -307,6 +317,9 @@ def test_burst_round_trip_full_size(dev, oracle_mod):
                                       data.data_ptr(), offs.data_ptr(), l32.data_ptr(),
                                       n, res.data_ptr(), ws.data_ptr(), ws.numel(), st) == 0
     assert int((res != OK).sum()) == 0
+    assert np.array_equal(res.cpu().numpy(), o_res)
+    assert np.array_equal(data.cpu().numpy(), o_sealed)  # every sealed byte
+    del o_sealed
 
     def decode(buf):
         res.fill_(9)
@@ -320,33 +333,38 @@ def test_burst_round_trip_full_size(dev, oracle_mod):
                                           st) == 0
         return res.clone(), iv, oseq, ofl
 
+    def against_oracle(buf, got, iv, oseq, ofl):
+        o_res, o_iv, o_seq, o_fl = oracle_mod.packet_decode_batch(
+            alg, key, True, ivlen, buf.cpu().numpy(), offs_h, lens_h,
+            nthreads=CPU_THREADS)
+        assert np.array_equal(got.cpu().numpy(), o_res)
+        assert np.array_equal(oseq.cpu().numpy().view(np.uint32), o_seq)
+        assert np.array_equal(ofl.cpu().numpy().view(np.uint32), o_fl)
+        ok = o_res == OK
+        assert np.array_equal(iv.cpu().numpy()[ok], o_iv[ok])
+        return o_res
+
     got, iv, oseq, ofl = decode(data)
     assert int((got != OK).sum()) == 0
+    against_oracle(data, got, iv, oseq, ofl)
     assert torch.equal(oseq, seq) and torch.equal(ofl, flags)
     want_iv = torch.empty_like(iv)
     assert L.net2_ph_to_iv_dev(seq.data_ptr(), flags.data_ptr(), n, ivlen,
                                want_iv.data_ptr(), st) == 0
     assert torch.equal(iv, want_iv)
-    # a sample against the oracle: the sealed hash field and the IV
-    rng = np.random.default_rng(42)
-    sample = rng.choice(n, 512, replace=False)
-    offs_h, lens_h = offs.cpu().numpy(), lens.cpu().numpy()
-    seq_h = seq.cpu().numpy().view(np.uint32)
-    iv_h = iv.cpu().numpy()
-    for i in sample:
-        a, b = int(offs_h[i]), int(offs_h[i]) + int(lens_h[i])
-        dg = data[a:b].cpu().numpy().tobytes()
-        assert dg[:8] == struct.pack(">II", int(seq_h[i]), PH_SIGNED | PH_ENCRYPTED)
-        assert dg[8:8 + hl] == oracle_mod.hmac(alg, key, dg[8 + hl:]), i
-        assert iv_h[i].tobytes() == oracle_mod.ph_to_iv(
-            int(seq_h[i]), PH_SIGNED | PH_ENCRYPTED, ivlen), i
+    # and the IVs of every header through the oracle's ph_to_iv batch
+    assert np.array_equal(iv.cpu().numpy(), oracle_mod.ph_to_iv_batch(
+        seq_h, fl_h, ivlen, nthreads=CPU_THREADS))
     # tamper with a chosen set: exactly those fail the hash compare
+    rng = np.random.default_rng(42)
     bad = np.sort(rng.choice(n, 4096, replace=False))
     pos = offs_h[bad] + 8 + rng.integers(0, lens_h[bad] - 8)
     t = data.clone()
     idx = torch.from_numpy(pos.astype(np.int64)).to(dev)
     t[idx] ^= 0x20
-    got, _, _, _ = decode(t)
+    got, iv, oseq, ofl = decode(t)
+    o_res = against_oracle(t, got, iv, oseq, ofl)
+    assert np.array_equal(np.nonzero(o_res)[0], bad)
     want = torch.zeros(n, dtype=torch.uint8, device=dev)
     want[torch.from_numpy(bad.astype(np.int64)).to(dev)] = BAD
     assert torch.equal(got, want)
