@@ -501,6 +501,7 @@ def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
         stop.set()
         sampler.join()
     launch_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    local_ms = elapsed * 1e3 / steps    # this rank's own, before the max
     if burst:   # every datagram of the synthetic burst is well-formed
         assert int((out != 0).sum()) == 0, f"{name}: datagrams not OK"
 
@@ -519,6 +520,7 @@ def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
         per_launch += n * (8 + 8 + DLEN[alg])
     res = {"n": n, "dlen": dlen, "payload": inp["payload"], "elapsed": elapsed,
            "ms_per_step": elapsed * 1e3 / steps, "launch_ms": launch_ms,
+           "ms_per_step_local": local_ms,
            "event_pairs": len(ev),
            "per_launch_bytes": per_launch,
            "sclk_during_mhz": (round(sum(samples) / len(samples)) if samples else None),
@@ -604,6 +606,75 @@ def unit_of(name):
     return "datagrams/s" if kind in ("dgram_verify", "burst_rx", "burst_tx") else "IVs/s" if kind == "ph_iv" else "digests/s"
 
 
+def pci_numa_node(pci):
+    try:
+        with open(f"/sys/bus/pci/devices/{pci}/numa_node") as f:
+            return int(f.read())
+    except (OSError, ValueError, TypeError):
+        return None
+
+
+def rank_record(rank, gpu, ms_per_step):
+    """What each rank contributes to an N>1 line: where it ran and its own
+    time per step (before the max over ranks)."""
+    return {"rank": rank, "host": gpu.get("host"), "pci": gpu.get("pci"),
+            "numa_node": pci_numa_node(gpu.get("pci")),
+            "ms_per_step": round(ms_per_step, 4)}
+
+
+def gather_ranks(rec, ws):
+    """Every rank's record, in rank order, on every rank."""
+    if ws == 1:
+        return [rec]
+    import torch.distributed as dist
+    out = [None] * ws
+    dist.all_gather_object(out, rec)
+    return out
+
+
+def scale_fields(ranks, backend):
+    """Fields of an N>1 line that say on which devices its ranks ran.  Under
+    RCCL ("nccl", the driver's scaling runs) two ranks on one GPU would make
+    the line's n_gpus a lie: that is an error, raised on every rank (all
+    hold the same records).  A gloo rehearsal that shares a device is
+    labelled so instead."""
+    keys = [(r["host"], r["pci"]) for r in ranks]
+    distinct = len(set(keys))
+    shared = distinct < len(ranks)
+    if shared and backend == "nccl":
+        dup = sorted({k for k in keys if keys.count(k) > 1})
+        raise SystemExit(f"bench.py: {len(ranks)} ranks but {distinct} distinct "
+                         f"GPUs (shared: {dup}); one process per GPU is required")
+    ms = [r["ms_per_step"] for r in ranks]
+    return {"distinct_devices": distinct,
+            "device_sharing": (f"shared device: {len(ranks)} ranks on {distinct} GPU(s), "
+                               "a rehearsal, not an N-GPU measurement") if shared
+            else "one GPU per rank",
+            "ms_per_step_ranks": {"min": min(ms), "max": max(ms)},
+            "ranks": ranks}
+
+
+def devices_label(ws, distinct):
+    return f"{ws} GPU(s)" if distinct == ws else \
+        f"{ws} ranks on {distinct} shared GPU(s)"
+
+
+def cpu_baseline_after_gpu(cfg, rank, ws, fn=None):
+    """cpu_baseline at any N, on rank 0 after every GPU step of the line is
+    done, so the 1/2/4/8-GPU lines each carry a same-box CPU figure (north
+    star).  The other ranks wait on the rendezvous store (a blocking socket
+    wait: no rank spins a CPU while rank 0 times the host)."""
+    import torch.distributed as dist
+    res = (fn or cpu_baseline)(cfg) if rank == 0 else None
+    if ws > 1:
+        store = dist.distributed_c10d._get_default_store()
+        if rank == 0:
+            store.set("net2_bench_cpu_baseline_done", "1")
+        else:
+            store.wait(["net2_bench_cpu_baseline_done"])
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -680,10 +751,20 @@ def main():
         line["roofline_valu"] = valu
     gpu["sclk_mhz_during_timed_steps"] = r["sclk_during_mhz"]
     line["gpu"] = gpu
+    ranks = gather_ranks(rank_record(rank, gpu, r["ms_per_step_local"]), ws)
+    if ws > 1:
+        sf = scale_fields(ranks, args.dist_backend)
+        line.update(sf)
+        line["config"]["parallelism"] = (
+            f"{ws} independent shards, no collective; " + sf["device_sharing"])
     if name == "c2" and not args.no_extras:
-        line["extra_configs"] = extra_configs(args, dev, probe, ws, rank)
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline and name in ("c2", "c3", "c4"):
-        line["cpu_baseline"] = cpu_baseline(cfg)
+        line["extra_configs"] = extra_configs(
+            args, dev, probe, ws, rank,
+            label=devices_label(ws, line.get("distinct_devices", ws)))
+    if not args.no_cpu_baseline and name in ("c2", "c3", "c4"):
+        cb = cpu_baseline_after_gpu(cfg, rank, ws)
+        if rank == 0:
+            line["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(line), flush=True)
     if ws > 1:
@@ -691,7 +772,7 @@ def main():
     return None
 
 
-def extra_configs(args, dev, probe, ws=1, rank=0):
+def extra_configs(args, dev, probe, ws=1, rank=0, label=None):
     """The other BASELINE.json configs, timed in the same invocation: at
     N=1, C3 (mixed lengths, binned) and C4 (SHA-512) device-resident with
     their rooflines, C1 (4096 x 1 KiB signed payloads) and the end-to-end
@@ -701,7 +782,7 @@ def extra_configs(args, dev, probe, ws=1, rank=0):
     out = {}
     if ws > 1:
         out["e2e"] = e2e_rate(steps=10, warmup=3, ws=ws, dev=dev,
-                              dist_backend=args.dist_backend)
+                              dist_backend=args.dist_backend, label=label)
         return out
     for name in ("c3", "c4"):
         r = time_device_config(name, dev, args.steps, min(args.warmup, 10),
@@ -754,7 +835,7 @@ def gpu_local_cpus(dev):
 
 
 def e2e_rate(steps, warmup, n=1 << 20, length=1024, ws=1, dev=None,
-             dist_backend="nccl"):
+             dist_backend="nccl", label=None):
     """C5's shape: 1 M x 1 KiB per GPU from pinned host memory -> the GPU ->
     digests back to pinned host memory, through net2_sha2_batch (each rank
     on its own GPU, max_devices 1); timed between barriers, max over ranks."""
@@ -770,12 +851,13 @@ def e2e_rate(steps, warmup, n=1 << 20, length=1024, ws=1, dev=None,
         os.sched_setaffinity(0, local)
     try:
         return _e2e_timed(steps, warmup, n, length, ws, dev, dist_backend,
-                          numa=bool(local))
+                          numa=bool(local), label=label or f"{ws} GPU(s)")
     finally:
         os.sched_setaffinity(0, saved)
 
 
-def _e2e_timed(steps, warmup, n, length, ws, dev, dist_backend, numa):
+def _e2e_timed(steps, warmup, n, length, ws, dev, dist_backend, numa,
+               label):
     import torch
     import torch.distributed as dist
     from ilias_net2_amd import _lib
@@ -796,14 +878,21 @@ def _e2e_timed(steps, warmup, n, length, ws, dev, dist_backend, numa):
     if ws > 1:
         dist.barrier()
     ms = (time.perf_counter() - t0) * 1e3 / steps
+    ms_local = ms
     if ws > 1:
         t = torch.tensor([ms], dtype=torch.float64,
                          device=dev if dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms = float(t[0])
+        t = torch.tensor([ms_local], dtype=torch.float64,
+                         device=dev if dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        ms_min = float(t[0])
     del host, outp
     return {"metric": "SHA-256 digests/s, 1 KiB packets from pinned host memory, "
-                      f"end to end (H2D, kernel, digests stored to host memory), {ws} GPU(s)",
+                      f"end to end (H2D, kernel, digests stored to host memory), {label}",
+            **({"ms_per_step_ranks": {"min": round(ms_min, 3), "max": round(ms, 3)}}
+               if ws > 1 else {}),
             "value": round(n * ws / (ms / 1e3), 1), "unit": "digests/s", "steps": steps,
             "n_gpus": ws, "ms_per_step": round(ms, 3),
             "workload": f"{ws} x 1M x 1 KiB, host -> GPU -> host via net2_sha2_batch, "
@@ -828,10 +917,21 @@ def run_e2e(args, ws, rank, dev):
     through net2_sha2_batch on this rank's device (PCIe-inclusive rate)."""
     import torch
     import torch.distributed as dist
+    gpu = gpu_info(dev)
+    sf = None
+    if ws > 1:
+        sf = scale_fields(gather_ranks(rank_record(rank, gpu, 0.0), ws),
+                          args.dist_backend)
     t0 = time.perf_counter()
     r = e2e_rate(args.steps, args.warmup, ws=ws, dev=dev,
-                 dist_backend=args.dist_backend)
+                 dist_backend=args.dist_backend,
+                 label=devices_label(ws, sf["distinct_devices"] if sf else ws))
     el = time.perf_counter() - t0
+    if sf:
+        r.update({"distinct_devices": sf["distinct_devices"],
+                  "device_sharing": sf["device_sharing"],
+                  "ranks": [dict(x, ms_per_step=None) for x in sf["ranks"]]})
+    r["gpu"] = gpu
     r.update({"n_gpus": ws, "warmup": args.warmup, "higher_is_better": True,
               "scaling": "weak", "vs_baseline": None, "dtype": "u32",
               "data": "synthetic random bytes in pinned host memory",

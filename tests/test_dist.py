@@ -84,3 +84,72 @@ def test_two_ranks_gloo():
     lens = synth.mixed_lengths(32, 2500)
     vdata, offs = synth.packed(33, lens)
     assert np.array_equal(vfull, oracle.batch(3, vdata, offsets=offs, lens=lens))
+
+
+# ---- the N>1 bench line --------------------------
+
+def _bench_worker(rank, world, port, q, pcis):
+    import torch.distributed as dist
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        gpu = {"host": "box-a", "pci": pcis[rank]}
+        ranks = bench.gather_ranks(bench.rank_record(rank, gpu, 1.0 + rank), world)
+        out = {"ranks": ranks, "gloo": bench.scale_fields(ranks, "gloo")}
+        try:
+            bench.scale_fields(ranks, "nccl")
+            out["nccl"] = "accepted"
+        except SystemExit as e:
+            out["nccl"] = "refused: " + str(e)
+        # cpu_baseline at N>1: rank 0 times the host after the GPU steps,
+        # the other ranks wait on the store (no spinning, no deadlock)
+        cb = bench.cpu_baseline_after_gpu({"n": 1}, rank, world,
+                                          fn=lambda cfg: {"value": 42.0, "cores": 16})
+        out["cpu_baseline"] = cb
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("shared", [True, False])
+def test_bench_rank_records_gloo(shared):
+    """Two gloo ranks build the N>1 line's device fields: every rank's PCI
+    id, host, NUMA node and own ms_per_step; min / max over ranks; two ranks
+    on one device are labelled "shared device" under gloo and refused under
+    RCCL (the driver's backend); distinct devices pass both.  rank 0 alone
+    carries cpu_baseline."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    pcis = ["0000:05:00.0", "0000:05:00.0"] if shared else ["0000:05:00.0", "0000:15:00.0"]
+    procs = [ctx.Process(target=_bench_worker, args=(r, 2, port, q, pcis))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank in (0, 1):
+        o = got[rank]
+        assert [r["rank"] for r in o["ranks"]] == [0, 1]
+        assert [r["pci"] for r in o["ranks"]] == pcis
+        assert all(set(r) >= {"host", "numa_node", "ms_per_step"} for r in o["ranks"])
+        g = o["gloo"]
+        assert g["ms_per_step_ranks"] == {"min": 1.0, "max": 2.0}
+        if shared:
+            assert g["distinct_devices"] == 1
+            assert g["device_sharing"].startswith("shared device")
+            assert o["nccl"].startswith("refused")
+        else:
+            assert g["distinct_devices"] == 2
+            assert g["device_sharing"] == "one GPU per rank"
+            assert o["nccl"] == "accepted"
+    assert got[0]["cpu_baseline"] == {"value": 42.0, "cores": 16}
+    assert got[1]["cpu_baseline"] is None
+    import bench
+    assert bench.devices_label(2, 1) == "2 ranks on 1 shared GPU(s)"
+    assert bench.devices_label(8, 8) == "8 GPU(s)"
