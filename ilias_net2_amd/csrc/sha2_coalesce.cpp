@@ -52,8 +52,14 @@ typedef std::chrono::steady_clock clk;
 
 constexpr int kMaxSlots = 16;
 constexpr size_t kInitialStage = 1u << 20;	/* grows on demand */
-/* staging grown past this for one large request is released once its
- * batch completes, so a few big hashiov / Update calls do not keep
+/* staging grown past this is released lazily: when a later batch on the
+ * same slot uses under a quarter of it.  A run of large requests (the
+ * 64 MiB pieces of a long SHA*Update or streamed hashiov, repeated 32 MiB
+ * calls) keeps reusing the slot's staging -- free slots are taken
+ * last-in-first-out, so a serial caller gets the same slot back -- instead
+ * of page-locking and freeing ~80 MiB per request (hipHostFree / hipFree
+ * also synchronise the device, stalling other slots' batches); the first
+ * small batch afterwards gives it back, so a few big calls do not keep
  * gigabytes page-locked for the life of the process */
 constexpr size_t kRetainStage = 16u << 20;
 constexpr size_t kMaxJobs = 1u << 16;		/* per batch */
@@ -427,8 +433,9 @@ int Coalescer::submit(int ordinal, const Request &r, int *hip_err)
 		futex_wake(w);		/* jp may be gone now; the address is inert */
 	}
 
-	/* the slot is still ours (not on free_): shrink outside the lock */
-	if (s.cap > kRetainStage)
+	/* the slot is still ours (not on free_): shrink outside the lock, once
+	 * oversized staging serves a batch that needs little of it */
+	if (s.cap > kRetainStage && s.used * 4 < s.cap)
 		s.free_stage();
 	lk.lock();
 	s.jobs.clear();
@@ -488,7 +495,7 @@ int Coalescer::launch_and_wait(Slot &s, int ordinal, int *hip_err)
 	std::vector<Job *> &jobs = s.jobs;
 	const size_t n = jobs.size();
 	size_t hdr_off, n256;
-	uint32_t waves, target, maxblk = 0;
+	uint32_t waves, target;
 	int wave;
 	const uint8_t *stage;
 	uint8_t *d_out;
@@ -518,9 +525,15 @@ int Coalescer::launch_and_wait(Slot &s, int ordinal, int *hip_err)
 	}
 	CO_TRY(hipHostGetDevicePointer((void **)&d_out, s.h_out, 0));
 	CO_TRY(hipHostGetDevicePointer((void **)&d_done, s.h_done, 0));
-	/* SHA-256 jobs first, then SHA-384/512; longest first within each,
-	 * so a wave's lanes share their trip count as far as possible */
+	/* Jobs of kWaveBlocks or more first (each takes a wave of its own,
+	 * whatever the batch size -- a lane would run one alone for a long
+	 * time); then SHA-256 jobs, then SHA-384/512, longest first within
+	 * each, so a wave's lanes share their trip count as far as possible */
 	std::sort(jobs.begin(), jobs.end(), [](const Job *a, const Job *b) {
+		const int la = a->desc.nblk >= kWaveBlocks;
+		const int lb = b->desc.nblk >= kWaveBlocks;
+		if (la != lb)
+			return la > lb;
 		const int fa = a->alg != 1, fb = b->alg != 1;
 		if (fa != fb)
 			return fa < fb;
@@ -532,7 +545,6 @@ int Coalescer::launch_and_wait(Slot &s, int ordinal, int *hip_err)
 		memcpy(s.h_stage + hdr_off + k * sizeof(Net2Job), &jobs[k]->desc,
 		    sizeof(Net2Job));
 		n256 += jobs[k]->alg == 1;
-		maxblk = std::max(maxblk, jobs[k]->desc.nblk);
 	}
 	if (!zerocopy_)
 		CO_TRY(hipMemcpyAsync(s.d_stage, s.h_stage,
@@ -540,15 +552,36 @@ int Coalescer::launch_and_wait(Slot &s, int ordinal, int *hip_err)
 		    s.stream));
 	stage = s.d_stage;
 	/* few jobs: a wave each (lower latency, the GPU is idle anyway);
-	 * many: a lane each */
-	wave = jobmode_ == 1 || (jobmode_ == 0 && (n <= kWaveJobsMax ||
-	    maxblk >= kWaveBlocks));
-	waves = wave ? (uint32_t)n :
-	    (uint32_t)((n256 + 63) / 64 + (n - n256 + 63) / 64);
-	target = s.done_base + waves;
-	CO_TRY(net2_launch_jobs(stage,
-	    reinterpret_cast<const Net2Job *>(stage + hdr_off), (uint32_t)n256,
-	    (uint32_t)(n - n256), d_out, d_done, wave, s.stream, job_chunk_));
+	 * many: a lane each -- except the long jobs at the front, which take
+	 * a wave each in a launch of their own, so one long request does not
+	 * switch a whole batch of small ones to the wave form */
+	wave = jobmode_ == 1 || (jobmode_ == 0 && n <= kWaveJobsMax);
+	if (wave) {
+		waves = (uint32_t)n;
+		target = s.done_base + waves;
+		CO_TRY(net2_launch_jobs(stage,
+		    reinterpret_cast<const Net2Job *>(stage + hdr_off),
+		    (uint32_t)n256, (uint32_t)(n - n256), d_out, d_done, 1,
+		    s.stream, job_chunk_));
+	} else {
+		size_t nl = 0, nl256 = 0;
+		if (jobmode_ == 0)
+			for (; nl < n && jobs[nl]->desc.nblk >= kWaveBlocks; nl++)
+				nl256 += jobs[nl]->alg == 1;
+		const size_t ns256 = n256 - nl256, ns512 = n - nl - ns256;
+		waves = (uint32_t)(nl + (ns256 + 63) / 64 + (ns512 + 63) / 64);
+		target = s.done_base + waves;
+		const Net2Job *hj =
+		    reinterpret_cast<const Net2Job *>(stage + hdr_off);
+		if (nl > 0)
+			CO_TRY(net2_launch_jobs(stage, hj, (uint32_t)nl256,
+			    (uint32_t)(nl - nl256), d_out, d_done, 1, s.stream,
+			    job_chunk_));
+		if (nl < n)
+			CO_TRY(net2_launch_jobs(stage, hj + nl, (uint32_t)ns256,
+			    (uint32_t)ns512, d_out + 64 * nl, d_done, 0, s.stream,
+			    job_chunk_));
+	}
 	CO_TRY(hipEventRecord(s.ev, s.stream));
 	{
 		/*

@@ -371,7 +371,9 @@ DeviceCtx *ctx_for(size_t idx)
  * the pack pool threads it starts, which inherit its mask -- is bound to the
  * CPUs of the device's node (sysfs numa_node of its PCI function, within the
  * process's CPUs) for the slice, and restored after.  NET2_SHA2_NUMA=0
- * turns it off.
+ * turns it off.  Slice 0 runs on the calling thread, so for the duration of
+ * a net2_sha2_batch call that thread's affinity is the node's CPUs (its own
+ * mask is restored before the call returns; include/net2/sha2_batch.h).
  */
 struct NumaPlace {
 	int node = -1;
@@ -399,6 +401,40 @@ bool parse_cpulist(const char *s, cpu_set_t *set)
 		s = *e == ',' ? e + 1 : e;
 	}
 	return true;
+}
+
+/*
+ * The CPUs this process may run on, whoever asks: the cgroup's effective
+ * cpuset when it is readable, else the affinity of the thread that loaded
+ * the library.  Not the calling thread's own mask: a caller pinned to one
+ * CPU must not narrow the placement every later slice of the device gets
+ * (the result is cached per device).
+ */
+cpu_set_t g_load_mask;
+bool g_load_mask_ok = false;
+
+__attribute__((constructor)) void capture_load_mask()
+{
+	g_load_mask_ok = sched_getaffinity(0, sizeof(g_load_mask),
+	    &g_load_mask) == 0;
+}
+
+bool process_cpus(cpu_set_t *out)
+{
+	char buf[4096];
+	FILE *f = fopen("/sys/fs/cgroup/cpuset.cpus.effective", "r");
+	if (f != nullptr) {
+		const bool ok = fgets(buf, sizeof(buf), f) != nullptr &&
+		    parse_cpulist(buf, out) && CPU_COUNT(out) > 0;
+		fclose(f);
+		if (ok)
+			return true;
+	}
+	if (g_load_mask_ok) {
+		*out = g_load_mask;
+		return true;
+	}
+	return sched_getaffinity(0, sizeof(*out), out) == 0;
 }
 
 const NumaPlace &numa_place(int ordinal)
@@ -434,8 +470,7 @@ const NumaPlace &numa_place(int ordinal)
 		FILE *f = fopen(path, "r");
 		cpu_set_t node_cpus, mine;
 		if (f != nullptr && fgets(buf, sizeof(buf), f) != nullptr &&
-		    parse_cpulist(buf, &node_cpus) &&
-		    sched_getaffinity(0, sizeof(mine), &mine) == 0) {
+		    parse_cpulist(buf, &node_cpus) && process_cpus(&mine)) {
 			CPU_AND(&p->cpus, &node_cpus, &mine);
 			p->have = CPU_COUNT(&p->cpus) > 0;
 		}
@@ -1055,10 +1090,41 @@ static int hashiov_streamed(int alg, const void *key, size_t keylen,
 		if ((rc = net2_sha2_ctx_update(halg, &c, blk, B)) != 0)
 			return rc;
 	}
-	for (size_t i = 0; i < iovcnt; i++)
-		if ((rc = net2_sha2_ctx_update(halg, &c, iov[i].iov_base,
-		    iov[i].iov_len)) != 0)
+	{
+		/* many small segments are gathered into requests of up to one
+		 * stream chunk (one GPU round trip each, not one per segment);
+		 * a segment of a chunk or more with nothing gathered goes as is */
+		const size_t chunk = std::max(long_message_bytes(), B);
+		std::vector<uint8_t> gbuf;
+		size_t have = 0;
+		for (size_t i = 0; i < iovcnt; i++) {
+			const uint8_t *q = (const uint8_t *)iov[i].iov_base;
+			size_t left = iov[i].iov_len;
+			if (have == 0 && left >= chunk) {
+				if ((rc = net2_sha2_ctx_update(halg, &c, q, left)) != 0)
+					return rc;
+				continue;
+			}
+			while (left > 0) {
+				if (gbuf.empty())
+					gbuf.resize(chunk);
+				const size_t take = std::min(left, chunk - have);
+				memcpy(gbuf.data() + have, q, take);
+				have += take;
+				q += take;
+				left -= take;
+				if (have == chunk) {
+					if ((rc = net2_sha2_ctx_update(halg, &c,
+					    gbuf.data(), have)) != 0)
+						return rc;
+					have = 0;
+				}
+			}
+		}
+		if (have > 0 && (rc = net2_sha2_ctx_update(halg, &c, gbuf.data(),
+		    have)) != 0)
 			return rc;
+	}
 	if ((rc = net2_sha2_ctx_final(halg, keyed ? inner : out, &c)) != 0 ||
 	    !keyed)
 		return rc;

@@ -57,9 +57,12 @@ int net2_hash_getkeylen(int alg);
  * Hash the concatenation of iov[0 .. iovcnt) with row alg and write the
  * digest (net2_hash_gethashlen(alg) bytes) to out, which holds outlen
  * bytes.  Returns 0, EINVAL (bad row, key length or outlen; an unkeyed row
- * given a key: hash-openssl.cc:199-200,227-228; a message of 2^32 - 64
- * blocks or more, i.e. about 256 GiB for SHA-256, 512 GiB for SHA-384/512),
- * ENOMEM, ENODEV or EIO.
+ * given a key: hash-openssl.cc:199-200,227-228), ENOMEM, ENODEV or EIO.
+ * A message of any length is accepted: one longer than
+ * NET2_SHA2_STREAM_CHUNK (default 64 MiB) goes to the GPU in requests of at
+ * most that size.  (Only with NET2_SHA2_STREAM_CHUNK set at or above the
+ * message size can a single request reach the 2^32 - 64 block limit of the
+ * coalescer, ~256 GiB for SHA-256, ~512 GiB for SHA-384/512: EINVAL.)
  * nil writes nothing and returns 0.  Runs on the calling thread's current
  * HIP device if it is a gfx950, else on the first gfx950; the current
  * device is unchanged on return.

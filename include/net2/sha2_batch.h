@@ -120,6 +120,10 @@ size_t net2_sha2_dev_var_workspace(uint64_t n);
  * payload (NET2_SHA2_SLICE_MIN_BYTES): a small batch stays on one device.
  * The device list starts at the calling thread's current HIP device (so
  * max_devices == 1 means "this device" for a one-process-per-GPU caller).
+ * NUMA: each slice's thread is bound to the CPUs of its GPU's node (within
+ * the process's cpuset) while the slice runs; the first slice runs on the
+ * calling thread, so that thread's affinity is the node's for the duration
+ * of the call and is restored before it returns (NET2_SHA2_NUMA=0: off).
  */
 int net2_sha2_batch(int alg, const void *base, const uint64_t *offsets,
     const uint32_t *lens, uint64_t stride, uint32_t fixed_len, uint64_t n,

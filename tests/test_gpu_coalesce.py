@@ -179,6 +179,66 @@ def test_hashiov_long_messages_streamed(L, oracle_mod, monkeypatch):
             assert out.raw[:dl] == want, (alg, n)
 
 
+def test_hashiov_streamed_gathers_small_segments(L, oracle_mod, monkeypatch):
+    """A long message made of many small iovecs goes to the GPU in requests
+    of about one stream chunk, not one per segment: 1,000
+    segments of 1-300 bytes with a 4 KiB chunk take ~40 launches, and the
+    digest / HMAC equal the oracle's."""
+    import ctypes as ct
+    from ilias_net2_amd._lib import IOVec
+    monkeypatch.setenv("NET2_SHA2_STREAM_CHUNK", "4096")
+    rng = np.random.default_rng(11)
+    sizes = rng.integers(1, 301, 1000)
+    m = rng.integers(0, 256, int(sizes.sum()), dtype=np.uint8).tobytes()
+    cuts = np.concatenate([[0], np.cumsum(sizes)])
+    bufs = [ct.create_string_buffer(m[a:b], b - a) for a, b in zip(cuts, cuts[1:])]
+    iov = (IOVec * len(bufs))(*[IOVec(ct.cast(b, ct.c_void_p), len(b)) for b in bufs])
+    for alg in (1, 3, 6):
+        key = bytes(range(64)) if alg == 6 else b""
+        kb = ct.create_string_buffer(key, max(len(key), 1))
+        out = ct.create_string_buffer(64)
+        c0, n0 = _stats(L)
+        assert L.net2_hashctx_hashiov(alg, kb if key else None, len(key), iov,
+                                      len(bufs), out, 64) == 0
+        c1, n1 = _stats(L)
+        want = oracle_mod.digest(alg, m) if alg <= 3 else oracle_mod.hmac(alg, key, m)
+        assert out.raw[:len(want)] == want, alg
+        assert n1 - n0 <= len(m) // 4096 + 8, (alg, n1 - n0)
+
+
+def test_long_job_in_a_batch_of_small_ones(L, oracle_mod):
+    """A long request (1,024 blocks or more) in a batch of many small ones
+    takes a wave of its own in a separate launch while the small ones keep
+    the lane form: 32 threads of 1 KiB calls and 2 threads
+    of 200 KiB calls at once, every digest against the oracle."""
+    import ctypes as ct
+    from ilias_net2_amd._lib import IOVec
+    rng = np.random.default_rng(12)
+    small = [rng.integers(0, 256, 1024, dtype=np.uint8).tobytes() for _ in range(32)]
+    big = [rng.integers(0, 256, 200 * 1024 + 17, dtype=np.uint8).tobytes()
+           for _ in range(2)]
+    bad = []
+
+    def run(msg, alg, reps):
+        b = ct.create_string_buffer(msg, len(msg))
+        iov = (IOVec * 1)(IOVec(ct.cast(b, ct.c_void_p), len(msg)))
+        want = oracle_mod.digest(alg, msg)
+        for _ in range(reps):
+            out = ct.create_string_buffer(64)
+            if L.net2_hashctx_hashiov(alg, None, 0, iov, 1, out, 64) != 0 or \
+                    out.raw[:len(want)] != want:
+                bad.append((alg, len(msg)))
+    ths = [threading.Thread(target=run, args=(m, 1 + 2 * (i % 2), 40))
+           for i, m in enumerate(small)]
+    ths += [threading.Thread(target=run, args=(m, 1 + 2 * i, 6))
+            for i, m in enumerate(big)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not bad, bad[:4]
+
+
 def _registry_key(key: bytes, alg: int) -> bytes:
     """RFC 2104: K' is K (hashed first if longer than the block) zero-padded
     to the block, so any zero extension of that up to the block gives the
