@@ -62,6 +62,8 @@ SIGNATURES = {
         ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
         ctypes.c_void_p]),
     "net2_sha2_dev_var_workspace": (ctypes.c_size_t, [ctypes.c_uint64]),
+    "net2_sha2_workspace_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t,
+                                                ctypes.c_void_p]),
     "net2_sha2_batch": (ctypes.c_int, [
         ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
         ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,

@@ -88,12 +88,18 @@ def digest_fixed(alg: int, data, stride: int, length: int, n: int, out=None,
 
 
 def var_workspace(n: int, device, stream=None):
-    """Binning scratch for n packets, allocated in ``stream``'s order."""
+    """Binning scratch for n packets, allocated and prepared
+    (net2_sha2_workspace_init) in ``stream``'s order."""
     import torch
     nbytes = _lib.lib().net2_sha2_dev_var_workspace(n)
-    with torch.cuda.stream(_launch_stream(stream, device)):
-        return torch.empty(((nbytes + 3) // 4,), dtype=torch.int32,
-                           device=device)
+    s = _launch_stream(stream, device)
+    with torch.cuda.stream(s):
+        ws = torch.empty(((nbytes + 3) // 4,), dtype=torch.int32,
+                         device=device)
+    check(_lib.lib().net2_sha2_workspace_init(ws.data_ptr(), ws.numel() * 4,
+                                              s.cuda_stream),
+          "net2_sha2_workspace_init")
+    return ws
 
 
 def _workspace(n: int, device, s, workspace=None):

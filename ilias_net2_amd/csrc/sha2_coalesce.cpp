@@ -525,13 +525,18 @@ int Coalescer::launch_and_wait(Slot &s, int ordinal, int *hip_err)
 	}
 	CO_TRY(hipHostGetDevicePointer((void **)&d_out, s.h_out, 0));
 	CO_TRY(hipHostGetDevicePointer((void **)&d_done, s.h_done, 0));
-	/* Jobs of kWaveBlocks or more first (each takes a wave of its own,
-	 * whatever the batch size -- a lane would run one alone for a long
-	 * time); then SHA-256 jobs, then SHA-384/512, longest first within
-	 * each, so a wave's lanes share their trip count as far as possible */
-	std::sort(jobs.begin(), jobs.end(), [](const Job *a, const Job *b) {
-		const int la = a->desc.nblk >= kWaveBlocks;
-		const int lb = b->desc.nblk >= kWaveBlocks;
+	/* In a lane-form batch, jobs of kWaveBlocks or more first (each takes
+	 * a wave of its own in a launch of their own -- a lane would run one
+	 * alone for a long time); then SHA-256 jobs, then SHA-384/512 (the
+	 * launches take each family as one run), longest first within each,
+	 * so a wave's lanes share their trip count as far as possible */
+	wave = jobmode_ == 1 || (jobmode_ == 0 && n <= kWaveJobsMax);
+	std::sort(jobs.begin(), jobs.end(), [wave, this](const Job *a,
+	    const Job *b) {
+		const int la = !wave && jobmode_ == 0 &&
+		    a->desc.nblk >= kWaveBlocks;
+		const int lb = !wave && jobmode_ == 0 &&
+		    b->desc.nblk >= kWaveBlocks;
 		if (la != lb)
 			return la > lb;
 		const int fa = a->alg != 1, fb = b->alg != 1;
@@ -555,7 +560,6 @@ int Coalescer::launch_and_wait(Slot &s, int ordinal, int *hip_err)
 	 * many: a lane each -- except the long jobs at the front, which take
 	 * a wave each in a launch of their own, so one long request does not
 	 * switch a whole batch of small ones to the wave form */
-	wave = jobmode_ == 1 || (jobmode_ == 0 && n <= kWaveJobsMax);
 	if (wave) {
 		waves = (uint32_t)n;
 		target = s.done_base + waves;

@@ -26,6 +26,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace net2 {
 namespace dev {
@@ -284,6 +285,17 @@ struct Sha512HF : Sha512 {
  * and re-aligned with v_alignbyte_b32.
  */
 enum { AMODE_A16 = 0, AMODE_A1 = 1, AMODE_A4 = 2 };
+/*
+ * NET2_ONEPATH (A/B): the variable-length and HMAC kernels take the A16
+ * block loads (global_load_dwordx4 at the block start) whatever the
+ * packet's alignment, relying on the unaligned access mode ROCm sets for
+ * gfx9+ global memory (tools/unaligned_probe.hip checks it on the box): one
+ * code path per kernel instead of three chosen per wave.  The tail block
+ * keeps its aligned-dword reads (it never touches a byte past the packet).
+ */
+#ifndef NET2_ONEPATH
+#define NET2_ONEPATH 0
+#endif
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 /*
@@ -1007,7 +1019,9 @@ __attribute__((amdgpu_waves_per_eu(VarWaves<H>::value))) void var_kernel(const u
 	if (sizeof(typename H::word) == 8)
 		k512_lds_fill();
 	const bool live = g < n;
-	const uint64_t i = live ? (perm ? (uint64_t)perm[g] : g) : 0;
+	uint64_t i = live ? (perm ? (uint64_t)perm[g] : g) : 0;
+	if (i >= n)	/* a corrupt workspace: never read out of bounds */
+		i = g;
 	const uint8_t *p = base + (live ? offsets[i] : 0);
 	const uint32_t len = live ? lens[i] : 0;
 	typename H::State st;
@@ -1016,7 +1030,7 @@ __attribute__((amdgpu_waves_per_eu(VarWaves<H>::value))) void var_kernel(const u
 	if constexpr (sizeof(typename H::word) == 8)
 		padtab = block_pad512(live, len);
 
-	if (__all((reinterpret_cast<uintptr_t>(p) & 15) == 0))
+	if (NET2_ONEPATH || __all((reinterpret_cast<uintptr_t>(p) & 15) == 0))
 		var_digest<H, AMODE_A16>(p, len, is384, kw, padtab, st);
 	else if (__all((reinterpret_cast<uintptr_t>(p) & 3) == 0))
 		var_digest<H, AMODE_A4>(p, len, is384, kw, padtab, st);
@@ -1238,6 +1252,8 @@ __attribute__((amdgpu_waves_per_eu(HmacWaves<H, MODE>::value))) void hmac_kernel
 	uint32_t len;
 	if (offsets != nullptr) {
 		i = live ? (perm ? (uint64_t)perm[g] : g) : 0;
+		if (i >= n)	/* a corrupt workspace: never out of bounds */
+			i = g;
 		p = base + (live ? offsets[i] : 0);
 		len = live ? lens[i] : 0;
 	} else {
@@ -1305,7 +1321,7 @@ __attribute__((amdgpu_waves_per_eu(HmacWaves<H, MODE>::value))) void hmac_kernel
 	}
 	typename H::State st;
 	const uintptr_t pa = reinterpret_cast<uintptr_t>(p);
-	const int amode = __all((pa & 15) == 0) ? AMODE_A16 :
+	const int amode = NET2_ONEPATH || __all((pa & 15) == 0) ? AMODE_A16 :
 	    __all((pa & 3) == 0) ? AMODE_A4 : AMODE_A1;
 	/* a variable-layout wave (SHA-256) or workgroup (SHA-512) of one
 	 * whole-block inner length (key block included) takes its inner pad
@@ -2004,6 +2020,261 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(
 }
 
 /*
+ * One-pass binning (NET2_BIN_ONEPASS): the count, the global prefix and the
+ * scatter in one launch, no memset.  A persistent grid of G <= 256
+ * workgroups (each loops over its 4,096-packet tiles):
+ *   1. LDS histogram of its tiles, added to the global histogram (one
+ *      device-scope atomic per touched bin);
+ *   2. a grid barrier on an arrival counter in the workspace header (the
+ *      last arriver flips `state` to GO);
+ *   3. every workgroup scans the global histogram (8 KiB) for the bin
+ *      bases, claims its ranges (one atomic per touched bin) and writes
+ *      perm from LDS ranks -- as bin_scatter_kernel, minus its launch.
+ * The workspace cleans up after itself: the histogram and claim counters
+ * come in two parities, each launch zeroes the one the next launch uses
+ * (the header's epoch selects), and the last workgroup to leave resets the
+ * counters and bumps the epoch.
+ *
+ * Never a hang, never a wrong order:
+ *   - a barrier that does not complete within NET2_BIN_TIMEOUT (the grid
+ *     not co-resident, e.g. beside many concurrent launches) is decided
+ *     ABORT by one compare-and-swap on `state`, which every workgroup then
+ *     follows: all write the identity order (perm[i] = i, hashing in
+ *     submission order: correct, only slower), and the header is marked for
+ *     re-initialisation;
+ *   - a workspace whose header is not initialised (the first use of a
+ *     caller's buffer unless net2_sha2_workspace_init ran, or after an
+ *     ABORT) takes the same identity order while workgroup 0 initialises
+ *     the header and both parities, so the next launch bins;
+ *   - the hash kernels clamp perm entries to [0, n) (a corrupt workspace
+ *     can cost digests, never an out-of-bounds access).
+ * The workspace must not be used by two launches at once (as before).
+ */
+#ifndef NET2_BIN_ONEPASS
+#define NET2_BIN_ONEPASS 1
+#endif
+#define NET2_BIN_MAGIC 0x4e45543242494e53ull	/* "NET2BINS" */
+#define NET2_BIN_GRID 256
+/* 50 ms of the 100 MHz s_memrealtime clock */
+#define NET2_BIN_TIMEOUT 5000000ull
+
+struct BinHdr {
+	uint64_t magic;
+	uint32_t epoch, arrive, leave, state;
+	uint32_t pad[NET2_BIN_HDR - 6];
+};
+static_assert(sizeof(BinHdr) == 4 * NET2_BIN_HDR, "header size");
+enum { BIN_UNDECIDED = 0, BIN_GO = 1, BIN_ABORT = 2 };
+
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t *p)
+{
+	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+/* perm[i] = i for this workgroup's tiles */
+__device__ __forceinline__ void bin_identity(uint32_t *perm, uint64_t n,
+    uint64_t ntiles)
+{
+	for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x)
+		for (int k = 0; k < NET2_BIN_ITEMS; k++) {
+			const uint64_t i = t * NET2_BIN_TILE + (uint64_t)k * 256 +
+			    threadIdx.x;
+			if (i < n)
+				perm[i] = (uint32_t)i;
+		}
+}
+
+__global__ __launch_bounds__(256) void bin_onepass_kernel(
+    const uint32_t *__restrict__ lens, uint64_t n, int blk_shift,
+    int lenbytes, uint32_t *__restrict__ ws, uint64_t timeout)
+{
+	__shared__ uint32_t cnt[NET2_SHA2_NBINS];
+	__shared__ uint32_t pre[NET2_SHA2_NBINS];
+	__shared__ uint32_t wsum[4];
+	__shared__ uint32_t bc[2];
+	BinHdr *h = reinterpret_cast<BinHdr *>(ws);
+	uint32_t *hist0 = ws + NET2_BIN_HDR;		/* [2][NBINS] */
+	uint32_t *cur0 = hist0 + 2 * NET2_SHA2_NBINS;	/* [2][NBINS] */
+	uint32_t *perm = ws + NET2_BIN_WS_WORDS;
+	const uint32_t G = gridDim.x;
+	const uint64_t ntiles = (n + NET2_BIN_TILE - 1) / NET2_BIN_TILE;
+
+	if (threadIdx.x == 0) {
+		bc[0] = __hip_atomic_load(&h->magic, __ATOMIC_ACQUIRE,
+		    __HIP_MEMORY_SCOPE_AGENT) == NET2_BIN_MAGIC;
+		bc[1] = ld_agent(&h->epoch);
+	}
+	__syncthreads();
+	if (!bc[0]) {
+		/* not initialised: submission order now, initialise for next */
+		bin_identity(perm, n, ntiles);
+		if (blockIdx.x == 0) {
+			for (uint32_t w = threadIdx.x; w < 4 * NET2_SHA2_NBINS;
+			    w += blockDim.x)
+				hist0[w] = 0;
+			if (threadIdx.x == 0) {
+				h->epoch = 0;
+				h->arrive = 0;
+				h->leave = 0;
+				h->state = BIN_UNDECIDED;
+			}
+			__threadfence();
+			__syncthreads();
+			if (threadIdx.x == 0)
+				__hip_atomic_store(&h->magic, NET2_BIN_MAGIC,
+				    __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+		}
+		return;
+	}
+	const uint32_t par = bc[1] & 1;
+	uint32_t *hist = hist0 + par * NET2_SHA2_NBINS;
+	uint32_t *cursor = cur0 + par * NET2_SHA2_NBINS;
+	/* the next launch's parity, zeroed across the grid */
+	for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+	    w < NET2_SHA2_NBINS; w += G * blockDim.x) {
+		hist0[(par ^ 1) * NET2_SHA2_NBINS + w] = 0;
+		cur0[(par ^ 1) * NET2_SHA2_NBINS + w] = 0;
+	}
+
+	/* 1: this workgroup's histogram, into the global one */
+	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
+		cnt[b] = 0;
+	__syncthreads();
+	for (uint64_t t = blockIdx.x; t < ntiles; t += G) {
+		const uint64_t i0 = t * NET2_BIN_TILE + threadIdx.x;
+		uint32_t len[NET2_BIN_ITEMS];
+		load_lens(lens, n, i0, len);
+#pragma unroll
+		for (int k = 0; k < NET2_BIN_ITEMS; k++)
+			if (i0 + (uint64_t)k * 256 < n)
+				atomicAdd(&cnt[bin_of(len[k], blk_shift, lenbytes,
+				    NET2_SHA2_NBINS)], 1u);
+	}
+	__syncthreads();
+	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
+		if (cnt[b] != 0)
+			__hip_atomic_fetch_add(&hist[b], cnt[b], __ATOMIC_RELAXED,
+			    __HIP_MEMORY_SCOPE_AGENT);
+	__threadfence();
+	__syncthreads();
+
+	/* 2: grid barrier, decided GO or ABORT exactly once */
+	if (threadIdx.x == 0) {
+		const uint32_t old = __hip_atomic_fetch_add(&h->arrive, 1u,
+		    __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+		if (old == G - 1) {
+			uint32_t exp = BIN_UNDECIDED;
+			__hip_atomic_compare_exchange_strong(&h->state, &exp,
+			    (uint32_t)BIN_GO, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+			    __HIP_MEMORY_SCOPE_AGENT);
+		}
+		const uint64_t t0 = wall_clock64();
+		uint32_t st;
+		while ((st = __hip_atomic_load(&h->state, __ATOMIC_ACQUIRE,
+		    __HIP_MEMORY_SCOPE_AGENT)) == BIN_UNDECIDED) {
+			if (wall_clock64() - t0 > timeout) {
+				uint32_t exp = BIN_UNDECIDED;
+				__hip_atomic_compare_exchange_strong(&h->state,
+				    &exp, (uint32_t)BIN_ABORT, __ATOMIC_ACQ_REL,
+				    __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+			}
+			__builtin_amdgcn_s_sleep(8);
+		}
+		bc[0] = st;
+	}
+	__syncthreads();
+	if (bc[0] == BIN_GO) {
+		/* 3: bin bases from the global histogram (8 bins per thread, a
+		 * shuffle scan per wave, the four wave totals), this
+		 * workgroup's ranges, then its packets' places */
+		constexpr int PER = NET2_SHA2_NBINS / 256;
+		const int lane = (int)__lane_id(), wave = (int)(threadIdx.x / 64);
+		uint32_t v[PER], sum = 0;
+#pragma unroll
+		for (int j = 0; j < PER; j++) {
+			v[j] = sum;
+			sum += ld_agent(&hist[threadIdx.x * PER + j]);
+		}
+		uint32_t x = sum;
+#pragma unroll
+		for (int off = 1; off < 64; off <<= 1) {
+			const uint32_t y = __shfl_up(x, off);
+			if (lane >= off)
+				x += y;
+		}
+		if (lane == 63)
+			wsum[wave] = x;
+		__syncthreads();
+		uint32_t base = x - sum;
+		for (int w = 0; w < wave; w++)
+			base += wsum[w];
+#pragma unroll
+		for (int j = 0; j < PER; j++)
+			pre[threadIdx.x * PER + j] = base + v[j];
+		__syncthreads();
+		for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
+			if (cnt[b] != 0)
+				cnt[b] = pre[b] + __hip_atomic_fetch_add(&cursor[b],
+				    cnt[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		__syncthreads();
+		for (uint64_t t = blockIdx.x; t < ntiles; t += G) {
+			const uint64_t i0 = t * NET2_BIN_TILE + threadIdx.x;
+			uint32_t len[NET2_BIN_ITEMS];
+			load_lens(lens, n, i0, len);
+#pragma unroll
+			for (int k = 0; k < NET2_BIN_ITEMS; k++) {
+				const uint64_t i = i0 + (uint64_t)k * 256;
+				if (i < n) {
+					const uint32_t pos = atomicAdd(&cnt[bin_of(len[k],
+					    blk_shift, lenbytes, NET2_SHA2_NBINS)], 1u);
+					if (pos < n)
+						perm[pos] = (uint32_t)i;
+				}
+			}
+		}
+	} else {
+		bin_identity(perm, n, ntiles);
+		if (threadIdx.x == 0)	/* re-initialise at the next launch */
+			__hip_atomic_store(&h->magic, 0ull, __ATOMIC_RELAXED,
+			    __HIP_MEMORY_SCOPE_AGENT);
+	}
+
+	/* the last workgroup out resets the barrier for the next launch */
+	__threadfence();
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		const uint32_t old = __hip_atomic_fetch_add(&h->leave, 1u,
+		    __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+		if (old == G - 1) {
+			h->arrive = 0;
+			h->leave = 0;
+			h->state = BIN_UNDECIDED;
+			h->epoch = bc[1] + 1;
+			__threadfence();
+		}
+	}
+}
+
+/* Prepares a binning workspace so its first launch bins (one workgroup). */
+__global__ __launch_bounds__(256) void bin_ws_init_kernel(uint32_t *ws)
+{
+	BinHdr *h = reinterpret_cast<BinHdr *>(ws);
+	for (uint32_t w = threadIdx.x; w < 4 * NET2_SHA2_NBINS; w += blockDim.x)
+		ws[NET2_BIN_HDR + w] = 0;
+	if (threadIdx.x == 0) {
+		h->epoch = 0;
+		h->arrive = 0;
+		h->leave = 0;
+		h->state = BIN_UNDECIDED;
+	}
+	__threadfence();
+	__syncthreads();
+	if (threadIdx.x == 0)
+		__hip_atomic_store(&h->magic, NET2_BIN_MAGIC, __ATOMIC_RELEASE,
+		    __HIP_MEMORY_SCOPE_AGENT);
+}
+
+/*
  * Tile-local binning (NET2_BIN_TILESORT=1; measured and NOT the default):
  * one launch, no global histogram -- workgroup t counting-sorts its own
  * tile of NET2_BIN_TILE_SORT packets by descending block count in LDS.
@@ -2181,6 +2452,13 @@ hipError_t net2_launch_fixed(int alg, const uint8_t *base, uint64_t stride,
 	return hipGetLastError();
 }
 
+hipError_t net2_bin_ws_init(uint32_t *ws, hipStream_t s)
+{
+	if (NET2_BIN_ONEPASS)
+		bin_ws_init_kernel<<<1, 256, 0, s>>>(ws);
+	return hipGetLastError();
+}
+
 /* Length-binned visiting order of a variable-length batch into ws. */
 hipError_t net2_bin_order(int alg, const uint32_t *lens, uint64_t n,
     uint32_t *ws, hipStream_t s)
@@ -2188,14 +2466,27 @@ hipError_t net2_bin_order(int alg, const uint32_t *lens, uint64_t n,
 	const bool s256 = alg == NET2_ALG_SHA256;
 	const int blk_shift = s256 ? 6 : 7;
 	const int lenbytes = s256 ? 8 : 16;
-	uint32_t *hist = ws;
-	uint32_t *cursor = ws + NET2_SHA2_NBINS;
-	uint32_t *perm = ws + 2 * NET2_SHA2_NBINS;
+	uint32_t *hist = ws + NET2_BIN_HDR;
+	uint32_t *cursor = hist + NET2_SHA2_NBINS;
+	uint32_t *perm = ws + NET2_BIN_WS_WORDS;
 	if (NET2_BIN_TILESORT) {
 		const unsigned g = (unsigned)((n + NET2_BIN_TILE_SORT - 1) /
 		    NET2_BIN_TILE_SORT);
 		bin_tile_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift, lenbytes,
 		    perm);
+		return hipGetLastError();
+	}
+	if (NET2_BIN_ONEPASS) {
+		const uint64_t tiles = (n + NET2_BIN_TILE - 1) / NET2_BIN_TILE;
+		const unsigned g = (unsigned)(tiles < NET2_BIN_GRID ? tiles :
+		    NET2_BIN_GRID);
+		/* NET2_BIN_TIMEOUT_US (tests): the barrier's timeout, default
+		 * 50 ms; 0 exercises the ABORT path */
+		const char *e = getenv("NET2_BIN_TIMEOUT_US");
+		const uint64_t to = e != nullptr && *e != '\0' ?
+		    strtoull(e, nullptr, 10) * 100 : NET2_BIN_TIMEOUT;
+		bin_onepass_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift,
+		    lenbytes, ws, to);
 		return hipGetLastError();
 	}
 	/* fused: cursor holds per-bin claim counters, zeroed with hist */
@@ -2227,7 +2518,7 @@ hipError_t net2_launch_var(int alg, const uint8_t *base,
 		hipError_t e = net2_bin_order(alg, lens, n, ws, s);
 		if (e != hipSuccess)
 			return e;
-		perm = ws + 2 * NET2_SHA2_NBINS;
+		perm = ws + NET2_BIN_WS_WORDS;
 	}
 	if (s256)
 		var_kernel<Sha256V><<<grid_for(n), 256, 0, s>>>(base, offsets,
@@ -2298,7 +2589,7 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 		hipError_t e = net2_bin_order(halg, lens, n, ws, s);
 		if (e != hipSuccess)
 			return e;
-		perm = ws + 2 * NET2_SHA2_NBINS;
+		perm = ws + NET2_BIN_WS_WORDS;
 	}
 	const unsigned grid = grid_for(n);
 	const bool padconst = offsets == nullptr && fixed_len % blk == 0;

@@ -19,20 +19,32 @@
  * SHA-256 blocks, so every legal payload gets its own bin. */
 #define NET2_SHA2_NBINS 2048
 
+/*
+ * Binning workspace (uint32 words): a 16-word header (the one-pass
+ * binning's state, sha2_kernels.hip bin_onepass_kernel), the histogram and
+ * claim counters in two parities (2 x 2 x NBINS), then perm[n].
+ */
+#define NET2_BIN_HDR 16
+#define NET2_BIN_WS_WORDS (NET2_BIN_HDR + 4 * NET2_SHA2_NBINS)
+
 /* Fixed-stride batch; base/out in device memory, async on s. */
 hipError_t net2_launch_fixed(int alg, const uint8_t *base, uint64_t stride,
     uint32_t len, uint64_t n, uint8_t *out, hipStream_t s);
 
 /*
  * Offset/length batch.  ws == NULL hashes in submission order (no binning);
- * otherwise ws holds 2 * NBINS + n uint32 words of scratch for the
+ * otherwise ws holds NET2_BIN_WS_WORDS + n uint32 words of scratch for the
  * length-binned order.
  */
 hipError_t net2_launch_var(int alg, const uint8_t *base,
     const uint64_t *offsets, const uint32_t *lens, uint64_t n, uint8_t *out,
     uint32_t *ws, hipStream_t s);
 
-/* Length-binned order (ws as above; perm = ws + 2 * NBINS). */
+/* Prepare ws (>= NET2_BIN_WS_WORDS words) so its first binning bins; an
+ * unprepared workspace hashes its first batch in submission order. */
+hipError_t net2_bin_ws_init(uint32_t *ws, hipStream_t s);
+
+/* Length-binned order (ws as above; perm = ws + NET2_BIN_WS_WORDS). */
 hipError_t net2_bin_order(int alg, const uint32_t *lens, uint64_t n,
     uint32_t *ws, hipStream_t s);
 

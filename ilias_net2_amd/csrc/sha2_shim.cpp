@@ -238,7 +238,10 @@ struct Slot {
 		HIP_TRY(hipMalloc((void **)&d_off, n * 8));
 		HIP_TRY(hipMalloc((void **)&d_len, n * 4));
 		HIP_TRY(hipMalloc((void **)&d_ws,
-		    (2 * NET2_SHA2_NBINS + n) * sizeof(uint32_t)));
+		    (NET2_BIN_WS_WORDS + n) * sizeof(uint32_t)));
+		/* prepared once, so the first variable-layout chunk bins too */
+		HIP_TRY(net2_bin_ws_init((uint32_t *)d_ws, nullptr));
+		HIP_TRY(hipStreamSynchronize(nullptr));
 		cap_in = in;
 		cap_n = n;
 		return 0;
@@ -902,7 +905,20 @@ NET2_EXPORT int net2_sha2_dev_fixed(int alg, const void *d_base,
 
 NET2_EXPORT size_t net2_sha2_dev_var_workspace(uint64_t n)
 {
-	return (2 * (size_t)NET2_SHA2_NBINS + (size_t)n) * sizeof(uint32_t);
+	return ((size_t)NET2_BIN_WS_WORDS + (size_t)n) * sizeof(uint32_t);
+}
+
+NET2_EXPORT int net2_sha2_workspace_init(void *d_ws, size_t ws_bytes,
+    void *stream)
+{
+	if (d_ws == nullptr || ws_bytes < net2_sha2_dev_var_workspace(0) ||
+	    ((uintptr_t)d_ws & 3) != 0)
+		return EINVAL;
+	int rc = check_current_device();
+	if (rc != 0)
+		return rc;
+	HIP_TRY(net2_bin_ws_init((uint32_t *)d_ws, (hipStream_t)stream));
+	return 0;
 }
 
 NET2_EXPORT int net2_sha2_dev_var(int alg, const void *d_base,
@@ -1334,7 +1350,7 @@ size_t burst_layout(uint64_t n, uint8_t *base, BurstWs *w)
 	uint8_t *vd = take(n);
 	uint32_t *sq = (uint32_t *)take(4 * n);
 	uint32_t *fl = (uint32_t *)take(4 * n);
-	uint32_t *bn = (uint32_t *)take((2 * (size_t)NET2_SHA2_NBINS + n) * 4);
+	uint32_t *bn = (uint32_t *)take(((size_t)NET2_BIN_WS_WORDS + n) * 4);
 	if (w != nullptr)
 		*w = { so, sl, st, vd, sq, fl, bn };
 	return at;

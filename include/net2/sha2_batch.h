@@ -94,9 +94,10 @@ int net2_sha2_dev_fixed(int alg, const void *d_base, uint64_t stride,
  * Device-resident batch, packed variable-length packets (config "1M x
  * mixed {64, 512, 1500} B"): packet i is d_base[d_offsets[i] ..
  * d_offsets[i] + d_lens[i]).  Lengths are binned on the device so lanes of
- * a wave share a block count; d_ws must hold
- * net2_sha2_dev_var_workspace(n) bytes of device memory (4-byte aligned)
- * or be NULL to hash in submission order (slower on mixed lengths).
+ * a wave share a block count (one binning launch); d_ws must hold
+ * net2_sha2_dev_var_workspace(n) bytes of device memory (4-byte aligned,
+ * see net2_sha2_workspace_init) or be NULL to hash in submission order
+ * (slower on mixed lengths).
  * Asynchronous on `stream`; d_ws must stay allocated until it completes.
  */
 int net2_sha2_dev_var(int alg, const void *d_base, const uint64_t *d_offsets,
@@ -105,6 +106,19 @@ int net2_sha2_dev_var(int alg, const void *d_base, const uint64_t *d_offsets,
 
 /* Bytes of scratch net2_sha2_dev_var needs for n packets. */
 size_t net2_sha2_dev_var_workspace(uint64_t n);
+
+/*
+ * Prepare a variable-layout workspace (net2_sha2_dev_var, the variable
+ * layouts of net2_hmac_dev / _sign_dev / _verify_dev), asynchronously on
+ * `stream`.  Optional: the binning keeps its state in the workspace and
+ * cleans up after itself, so a workspace reused call after call needs this
+ * at most once; an unprepared one (fresh memory) hashes its first batch in
+ * submission order -- same digests, only without the length binning --
+ * while it prepares itself.  A workspace must not serve two launches that
+ * may run at once.  0, EINVAL (NULL, misaligned or smaller than
+ * net2_sha2_dev_var_workspace(0)), ENODEV or EIO.
+ */
+int net2_sha2_workspace_init(void *d_ws, size_t ws_bytes, void *stream);
 
 /*
  * Host-memory batch, end to end: packets are read from host memory (DMA'd

@@ -7,5 +7,5 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/gputest.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 400 python -u tools/latency_long.py > gpurun_out/latency_long.jsonl 2> gpurun_out/latency_long.err
 rc=$?; echo "latency rc=$rc"; cat gpurun_out/latency_long.jsonl | cut -c1-300; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 60 ./tools/unaligned_probe > gpurun_out/unaligned_probe.json; echo "probe rc=$?"; cat gpurun_out/unaligned_probe.json
+
 bash tools/gpu_dist.sh
