@@ -45,6 +45,62 @@ iov_len(const struct iovec *iov, size_t n)
 }
 
 /*
+ * A few long payloads: one net2_hashctx_hashiov per payload, submitted from
+ * as many threads at once, so the request coalescer runs them as one batch
+ * in its wave-per-message form (the 64 lanes expand a message's schedules
+ * in parallel; a lone 64 KiB SHA-512 payload: ~2.0 ms, against ~3.6 ms as
+ * one lane of a net2_sha2_batch, profiles/round4/latency_long.jsonl).
+ */
+#define NET2_SC_FEW 16			/* the coalescer's wave-form batch */
+#define NET2_SC_LONG_BYTES 8192		/* mean payload above which it pays */
+
+struct one_hash {
+	const struct payload_ref *p;
+	int alg, rc;
+};
+
+static void *
+one_hash_run(void *arg)
+{
+	struct one_hash *o = arg;
+
+	o->rc = net2_hashctx_hashiov(o->alg, NULL, 0, o->p->iov, o->p->iovcnt,
+	    o->p->digest, 64);
+	return NULL;
+}
+
+static int
+hash_few_long(struct payload_ref *p, size_t np, int alg)
+{
+	struct one_hash job[NET2_SC_FEW];
+	pthread_t tid[NET2_SC_FEW];
+	int started[NET2_SC_FEW];
+	size_t m = 0;
+	int rc = 0;
+
+	for (size_t i = 0; i < np; i++)
+		if (p[i].alg == alg)
+			job[m++] = (struct one_hash){ &p[i], alg, 0 };
+	for (size_t k = 1; k < m; k++)
+		started[k] = pthread_create(&tid[k], NULL, one_hash_run,
+		    &job[k]) == 0;
+	one_hash_run(&job[0]);
+	for (size_t k = 1; k < m; k++) {
+		if (started[k])
+			pthread_join(tid[k], NULL);
+		else
+			one_hash_run(&job[k]);	/* could not start a thread */
+	}
+	for (size_t k = 0; k < m; k++)
+		if (job[k].rc != 0) {
+			if (*job[k].p->rc == 0)
+				*job[k].p->rc = job[k].rc;
+			rc = rc ? rc : job[k].rc;
+		}
+	return rc;
+}
+
+/*
  * Hash every payload of algorithm alg in one net2_sha2_batch call.
  * Single-segment payloads are passed in place, as offsets from the lowest
  * payload address; multi-segment ones are gathered first.
@@ -69,6 +125,14 @@ hash_group(struct payload_ref *p, size_t np, int alg)
 	}
 	if (m == 0)
 		return 0;
+	if (m <= NET2_SC_FEW) {
+		size_t total = 0;
+		for (size_t i = 0; i < np; i++)
+			if (p[i].alg == alg)
+				total += iov_len(p[i].iov, p[i].iovcnt);
+		if (total >= m * (size_t)NET2_SC_LONG_BYTES)
+			return hash_few_long(p, np, alg);
+	}
 	offs = malloc(m * sizeof(*offs));
 	lens = malloc(m * sizeof(*lens));
 	dig = malloc(m * (size_t)hl);

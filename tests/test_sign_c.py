@@ -126,3 +126,36 @@ def test_hash_tick_4096_x_1k_against_oracle(oracle_mod):
         for i in idx:
             assert reqs[i].rc == 0 and reqs[i].digestlen == hl, i
             assert bytes(reqs[i].digest[:hl]) == want[i].tobytes(), i
+
+
+@pytest.mark.gpu
+def test_hash_tick_few_long_payloads(oracle_mod):
+    """A tick of a few long payloads (the reference's maximum, 65,536 B,
+    src/carver.c:150,161, and above) takes the coalescer's wave-per-message
+    form (one request per payload, submitted at once); digests against the
+    oracle, multi-segment payloads included."""
+    import numpy as np
+    import ilias_net2_amd._lib as L
+    from synth import random_bytes
+    L.lib()
+    lib = ctypes.CDLL(LIB)
+    lib.net2_sc_hash_tick.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    sizes = [65536, 70001, 65536, 100000, 9000]
+    datas = [random_bytes(50 + i, n) for i, n in enumerate(sizes)]
+    iov = (L.IOVec * (2 * len(sizes)))()
+    reqs = (HashReq * len(sizes))()
+    for i, d in enumerate(datas):
+        cut = 1000 if i % 2 else len(d)
+        iov[2 * i].iov_base = d.ctypes.data
+        iov[2 * i].iov_len = cut
+        iov[2 * i + 1].iov_base = d.ctypes.data + cut
+        iov[2 * i + 1].iov_len = len(d) - cut
+        reqs[i].payload = ctypes.addressof(iov) + 2 * i * ctypes.sizeof(L.IOVec)
+        reqs[i].iovcnt = 2
+        reqs[i].hash_alg = (1, 3, 2, 3, 1)[i]
+    assert lib.net2_sc_hash_tick(reqs, len(sizes), 4) == 0
+    for i, d in enumerate(datas):
+        alg = reqs[i].hash_alg
+        want = oracle_mod.digest(alg, d.tobytes())
+        assert reqs[i].rc == 0 and reqs[i].digestlen == len(want), i
+        assert bytes(reqs[i].digest[:len(want)]) == want, i
