@@ -746,49 +746,10 @@ struct Rounds512<80> {
 	    uint64_t (&)[16], const lds_k64 *) {}
 };
 
-/*
- * The chaining value a compression adds back at its end (the feed-forward,
- * src/sha2.c:726-733), parked in LDS instead of 16 VGPRs (STLDS): word k of
- * lane l at st512_lds[k][l], so a wave's 64 ds_write_b64 / ds_read_b64 hit
- * consecutive banks.  The rounds then run on the state registers
- * themselves.  The reads go through an opaque zero offset (the compiler
- * cannot forward the stored registers to them) behind a scheduling barrier
- * (it cannot hoist them above the rounds either), so nothing of the old
- * state stays in VGPRs across the 80 rounds.  16 KiB per 256-lane
- * workgroup.
- */
-typedef __attribute__((address_space(3))) uint64_t lds_st64;
-__shared__ uint64_t st512_lds[8][256];
-
-__device__ __forceinline__ void st512_save(const uint64_t (&st)[8])
-{
-#pragma unroll
-	for (int i = 0; i < 8; i++)
-		st512_lds[i][threadIdx.x] = st[i];
-}
-
-__device__ __forceinline__ void st512_add_saved(uint64_t (&st)[8])
-{
-	uint32_t z;
-	asm volatile("s_mov_b32 %0, 0" : "=s"(z));
-	const lds_st64 *b = (const lds_st64 *)&st512_lds[0][0] + z;
-	__builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-	for (int i = 0; i < 8; i++)
-		st[i] += b[i * 256 + threadIdx.x];
-}
-
 /* SHA512Transform (src/sha2.c:663-734) on registers. */
-template <bool STLDS = false>
 __device__ __forceinline__ void compress512(uint64_t (&st)[8],
     uint64_t (&w)[16])
 {
-	if (STLDS) {
-		st512_save(st);
-		Rounds512<0>::run(st, w, k512_base());
-		st512_add_saved(st);
-		return;
-	}
 	uint64_t s[8];
 #pragma unroll
 	for (int i = 0; i < 8; i++)
@@ -821,16 +782,9 @@ struct RoundsKW512<80> {
 	    const uint64_t *, const lds_k64 *) {}
 };
 
-template <bool STLDS = false>
 __device__ __forceinline__ void compress512_kw(uint64_t (&st)[8],
     const uint64_t *kw)
 {
-	if (STLDS) {
-		st512_save(st);
-		RoundsKW512<0>::run(st, kw, k512_base());
-		st512_add_saved(st);
-		return;
-	}
 	uint64_t s[8];
 #pragma unroll
 	for (int i = 0; i < 8; i++)

@@ -47,7 +47,6 @@ struct Sha256T {
 	static constexpr bool PAIR = PAIR_;
 	static constexpr bool DRAIN = DRAIN_;	/* prio_remaining */
 	static constexpr bool GLDS = false;	/* absorb: LDS-DMA staging */
-	static constexpr bool STLDS = false;	/* compress512: LDS feed-forward */
 	typedef uint32_t word;
 	static constexpr int BLOCK = 64;	/* bytes per block */
 	static constexpr int NW32 = 16;		/* 32-bit words per block */
@@ -140,18 +139,8 @@ typedef Sha256T<NET2_HMAC_ASM != 0, NET2_HMAC_U2 != 0, NET2_HMAC_PAIR != 0> Sha2
 #ifndef NET2_SHA512_DRAIN
 #define NET2_SHA512_DRAIN 1
 #endif
-/*
- * NET2_STLDS512 (bit per kernel family, as NET2_GLDS512: 1 variable-length
- * SHA-512, 2 the variable-length HMAC-SHA512 kernels incl. bursts, 8 the
- * fixed SHA-512 kernel): the feed-forward copy of the state lives in LDS
- * (compress512<true>, sha2_device.h), 16 VGPRs fewer.
- */
-#ifndef NET2_STLDS512
-#define NET2_STLDS512 0x0
-#endif
 struct Sha512 {
 	static constexpr bool ASM = false;
-	static constexpr bool STLDS = (NET2_STLDS512 & 8) != 0;
 	/* no prefetch: nothing to ping-pong (NET2_FIXED512_PF=1: the two-block
 	 * ping-pong prefetch, A/B only) */
 	static constexpr bool U2 = NET2_FIXED512_PF != 0;
@@ -174,20 +163,14 @@ struct Sha512 {
 		for (int i = 0; i < 8; i++)
 			st[i] = is384 ? IV384[i] : IV512[i];
 	}
-	template <bool L>
-	__device__ __forceinline__ static void compress_t(State &st,
+	__device__ __forceinline__ static void compress(State &st,
 	    uint32_t (&b)[32])
 	{
 		uint64_t w[16];
 #pragma unroll
 		for (int i = 0; i < 16; i++)
 			w[i] = mk64(b[2 * i + 1], b[2 * i]);
-		compress512<L>(st, w);
-	}
-	__device__ __forceinline__ static void compress(State &st,
-	    uint32_t (&b)[32])
-	{
-		compress_t<STLDS>(st, b);
+		compress512(st, w);
 	}
 	__device__ __forceinline__ static void out_words(const State &st,
 	    uint32_t (&o)[16], int)
@@ -218,12 +201,6 @@ struct Sha512 {
 struct Sha512V : Sha512 {
 	static constexpr bool DRAIN = false;
 	static constexpr bool GLDS = (NET2_GLDS512 & 1) != 0;
-	static constexpr bool STLDS = (NET2_STLDS512 & 1) != 0;
-	__device__ __forceinline__ static void compress(State &st,
-	    uint32_t (&b)[32])
-	{
-		compress_t<STLDS>(st, b);
-	}
 	static constexpr bool U2 = NET2_VAR512_PF != 0 && !GLDS;
 	static constexpr bool PREFETCH = NET2_VAR512_PF != 0 && !GLDS;
 };
@@ -237,12 +214,6 @@ struct Sha512V : Sha512 {
 #endif
 struct Sha512J : Sha512 {
 	static constexpr bool DRAIN = false;
-	static constexpr bool STLDS = false;	/* 64-lane workgroups */
-	__device__ __forceinline__ static void compress(State &st,
-	    uint32_t (&b)[32])
-	{
-		compress_t<false>(st, b);
-	}
 	static constexpr bool U2 = NET2_JOB512_PF != 0;
 	static constexpr bool PREFETCH = NET2_JOB512_PF != 0;
 };
@@ -253,24 +224,12 @@ struct Sha512J : Sha512 {
 struct Sha512H : Sha512 {
 	static constexpr bool DRAIN = false;
 	static constexpr bool GLDS = (NET2_GLDS512 & 2) != 0;
-	static constexpr bool STLDS = (NET2_STLDS512 & 2) != 0;
-	__device__ __forceinline__ static void compress(State &st,
-	    uint32_t (&b)[32])
-	{
-		compress_t<STLDS>(st, b);
-	}
 	static constexpr bool U2 = NET2_HMAC512_PF != 0 && !GLDS;
 	static constexpr bool PREFETCH = NET2_HMAC512_PF != 0 && !GLDS;
 };
 /* ... and for the fixed-layout HMAC-SHA512 kernel (drain priority kept) */
 struct Sha512HF : Sha512 {
 	static constexpr bool GLDS = (NET2_GLDS512 & 4) != 0;
-	static constexpr bool STLDS = false;
-	__device__ __forceinline__ static void compress(State &st,
-	    uint32_t (&b)[32])
-	{
-		compress_t<false>(st, b);
-	}
 };
 
 /* ---- message loading ------------------------------------------------- */
@@ -719,7 +678,7 @@ __device__ __forceinline__ void finish(const uint8_t *p, uint32_t len,
 			compress256_kw<H::ASM>(*reinterpret_cast<uint32_t(*)[8]>(&st),
 			    reinterpret_cast<const uint32_t *>(kw));
 		else
-			compress512_kw<H::STLDS>(*reinterpret_cast<uint64_t(*)[8]>(&st),
+			compress512_kw(*reinterpret_cast<uint64_t(*)[8]>(&st),
 			    reinterpret_cast<const uint64_t *>(kw));
 		return;
 	}
