@@ -39,6 +39,19 @@ class SignReq(ctypes.Structure):
                 ("out", ctypes.POINTER(Sig)), ("rc", ctypes.c_int)]
 
 
+class HashReq(ctypes.Structure):
+    """struct net2_sc_hash_req (include/net2/signed_carver.h)."""
+
+
+HashReq._fields_ = [("payload", ctypes.c_void_p), ("iovcnt", ctypes.c_size_t),
+                    ("hash_alg", ctypes.c_int),
+                    ("done", ctypes.CFUNCTYPE(None, ctypes.POINTER(HashReq),
+                                              ctypes.c_void_p)),
+                    ("arg", ctypes.c_void_p), ("rc", ctypes.c_int),
+                    ("digestlen", ctypes.c_uint32),
+                    ("digest", ctypes.c_uint8 * 64)]
+
+
 class ValReq(ctypes.Structure):
     """struct net2_sc_validate_req (include/net2/signed_carver.h)."""
     _fields_ = [("payload", ctypes.POINTER(IOV)), ("iovcnt", ctypes.c_size_t),
@@ -183,6 +196,26 @@ def stages():
                 "payloads_per_s": n / t_vt, "ms": t_vt * 1e3})
     for i in range(n):
         S.net2x_signature_deinit(ctypes.byref(outs[i]))
+
+    # the hash-only tick the reference's own sign layer binds to
+    # (net2_sc_hash_req; the callbacks, here none, would run its ECDSA):
+    # 4096 payloads' SHA-512 digests, one GPU batch
+    hreqs = (HashReq * n)()
+    for i in range(n):
+        hreqs[i].payload = ctypes.addressof(iovs[i])
+        hreqs[i].iovcnt = 1
+        hreqs[i].hash_alg = 3
+
+    def hash_tick():
+        rc = S.net2_sc_hash_tick(hreqs, ctypes.c_size_t(n), threads)
+        assert rc == 0, rc
+    t_ht = timeit(hash_tick)
+    want = oracle.batch(3, data, stride=length, length=length, n=n)
+    assert all(bytes(hreqs[i].digest) == want[i].tobytes() for i in range(0, n, 97))
+    res.append({"key": "sc_hash_tick",
+                "stage": f"net2_sc_hash_tick: {n} x 1 KiB SHA512 digests, one tick (the "
+                         "reference binding's hash step; its ECDSA runs in the callbacks)",
+                "payloads_per_s": n / t_ht, "ms": t_ht * 1e3})
     return res
 
 

@@ -82,7 +82,7 @@ def main():
 
     # ---- one-payload ticks ----------------------------------------------
     import bench_sign as bs
-    from test_sign_c import HashReq
+    HashReq = bs.HashReq
     S = ctypes.CDLL(os.path.join(ROOT, "ilias_net2_amd", "libnet2_sign.so"))
     S.net2x_signctx_privnew.restype = ctypes.c_void_p
     S.net2x_signature_deinit.restype = None
