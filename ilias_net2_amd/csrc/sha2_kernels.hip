@@ -245,15 +245,20 @@ struct Sha512HF : Sha512 {
  */
 enum { AMODE_A16 = 0, AMODE_A1 = 1, AMODE_A4 = 2 };
 /*
- * NET2_ONEPATH (A/B): the variable-length and HMAC kernels take the A16
- * block loads (global_load_dwordx4 at the block start) whatever the
- * packet's alignment, relying on the unaligned access mode ROCm sets for
- * gfx9+ global memory (tools/unaligned_probe.hip checks it on the box): one
- * code path per kernel instead of three chosen per wave.  The tail block
- * keeps its aligned-dword reads (it never touches a byte past the packet).
+ * NET2_ONEPATH: the variable-length and HMAC kernels take the A16 block
+ * loads (global_load_dwordx4 at the block start) whatever the packet's
+ * alignment, relying on the unaligned access mode ROCm sets for gfx9+
+ * global memory (tools/unaligned_probe.hip: every byte offset reads the
+ * right bytes on gfx950, profiles/round4/unaligned_probe.json): one code
+ * path per kernel instead of three chosen per wave (A16 / A4 / A1).  The
+ * tail block keeps its aligned-dword reads (it never touches a byte past
+ * the packet).  A misaligned dwordx4 costs the memory pipeline more (a
+ * pure load stream at byte offset 1: 59 against 22 us), which these
+ * VALU-bound kernels hide: RX verify +1.7 / +2.2 %, burst RX +1.4 /
+ * +0.8 %, the rest within +-0.5 % (profiles/round4/ab_*.txt).
  */
 #ifndef NET2_ONEPATH
-#define NET2_ONEPATH 0
+#define NET2_ONEPATH 1
 #endif
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));

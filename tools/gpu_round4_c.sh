@@ -8,4 +8,4 @@ for c in c3 burst_rx; do
   rc=$?; echo "trace $c rc=$rc"; [ $rc -ne 0 ] && exit $rc
   f=$(find gpurun_out/prof_$c -name "*kernel_stats.csv" | head -1); cut -c1-160 $f | head -12
 done
-CFGS=${CFGS:-"c3 c3_512 hmac512_verify_mtu burst_rx c4"} REPS=${REPS:-"1 2"} bash tools/gpu_ab_lib.sh
+CFGS=${CFGS:-"c3 c3_512 hmac_mtu hmac_verify_mtu hmac512_mtu hmac512_verify_mtu burst_rx burst_tx"} REPS=${REPS:-"1 2"} bash tools/gpu_ab_lib.sh
