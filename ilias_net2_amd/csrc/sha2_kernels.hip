@@ -25,6 +25,7 @@
 #include "sha2_launch.h"
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -972,16 +973,14 @@ struct VarWaves {
 	static constexpr int value = sizeof(typename H::word) == 8 ?
 	    NET2_VAR512_WAVES : NET2_VAR256_WAVES;
 };
+/* One packet of var_kernel: binned position g (SHA-512: block_pad512 is a
+ * workgroup barrier, so every thread calls this equally often). */
 template <class H>
-__global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(VarWaves<H>::value))) void var_kernel(const uint8_t *__restrict__ base,
-    const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
-    const uint32_t *__restrict__ perm, uint64_t n, uint8_t *__restrict__ out,
-    uint32_t dlen, int is384)
+__device__ __forceinline__ void var_item(uint64_t g,
+    const uint8_t *__restrict__ base, const uint64_t *__restrict__ offsets,
+    const uint32_t *__restrict__ lens, const uint32_t *__restrict__ perm,
+    uint64_t n, uint8_t *__restrict__ out, uint32_t dlen, int is384)
 {
-	const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	if (sizeof(typename H::word) == 8)
-		k512_lds_fill();
 	const bool live = g < n;
 	uint64_t i = live ? (perm ? (uint64_t)perm[g] : g) : 0;
 	if (i >= n)	/* a corrupt workspace: never read out of bounds */
@@ -1011,6 +1010,62 @@ __attribute__((amdgpu_waves_per_eu(VarWaves<H>::value))) void var_kernel(const u
 		store_digest<48>(out + i * 48, o);
 	else
 		store_digest<H::DLEN>(out + i * H::DLEN, o);
+}
+
+/*
+ * NET2_SHORT2: in a binned batch, the lanes of the short tail (packets of at
+ * most two blocks, counted by the binning: split[0]) take two packets each,
+ * so half as many waves run it and each workgroup's fixed start -- for the
+ * HMAC kernels the constant table, key block and barriers -- serves twice
+ * the packets.  Workgroup-aligned, so every thread of a workgroup loops the
+ * same number of times.  Returns the number of packets (0: the whole
+ * workgroup exits, its packets are taken by lanes below) and the second
+ * position.
+ */
+#ifndef NET2_SHORT2
+#define NET2_SHORT2 0
+#endif
+/* SHA-512 kernels only: the second packet costs the SHA-256 kernels a few
+ * VGPRs, which at 96 is their fifth wave */
+template <class H>
+struct Short2 {
+	static constexpr bool value = NET2_SHORT2 != 0 &&
+	    sizeof(typename H::word) == 8;
+};
+template <class H>
+__device__ __forceinline__ int short2_reps(const uint32_t *split,
+    const uint32_t *perm, uint64_t n, uint64_t g, uint64_t &g2)
+{
+	if (!Short2<H>::value || perm == nullptr || split == nullptr)
+		return 1;
+	const uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x;
+	const uint64_t s0 = ((uint64_t)split[0] + 255) / 256 * 256;
+	if (s0 >= n || b0 < s0)
+		return 1;
+	const uint64_t half = ((n - s0 + 1) / 2 + 255) / 256 * 256;
+	if (b0 >= s0 + half)
+		return 0;
+	g2 = g + half;
+	return 2;
+}
+
+template <class H>
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(VarWaves<H>::value))) void var_kernel(const uint8_t *__restrict__ base,
+    const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
+    const uint32_t *__restrict__ perm, uint64_t n, uint8_t *__restrict__ out,
+    uint32_t dlen, int is384, const uint32_t *__restrict__ split)
+{
+	const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	uint64_t g2 = 0;
+	const int reps = short2_reps<H>(split, perm, n, g, g2);
+	if (reps == 0)
+		return;
+	if (sizeof(typename H::word) == 8)
+		k512_lds_fill();
+	var_item<H>(g, base, offsets, lens, perm, n, out, dlen, is384);
+	if (Short2<H>::value && reps == 2)
+		var_item<H>(g2, base, offsets, lens, perm, n, out, dlen, is384);
 }
 
 /* ---- HMAC (RFC 2104) ------------------------------------------------------ */
@@ -1146,6 +1201,7 @@ __device__ __forceinline__ uint32_t load_be32_bytes(const uint8_t *p)
 #define NET2_VERIFY_WORDS 1
 #endif
 
+
 /*
  * Occupancy of the SHA-512 HMAC kernels: NET2_HMAC512_W5 has bit MODE set
  * for the modes compiled for 5 waves per SIMD (96 VGPRs, some scratch
@@ -1167,49 +1223,22 @@ struct HmacWaves {
 	static constexpr int value = !H::GLDS && ((sizeof(typename H::word) == 8 ?
 	    NET2_HMAC512_W5 : NET2_HMAC256_W5) >> MODE & 1) ? 5 : 1;
 };
-template <class H, bool PADCONST, int MODE = HMAC_DIGESTS>
-__global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(HmacWaves<H, MODE>::value))) void hmac_kernel(const uint8_t *__restrict__ base,
-    const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
-    const uint32_t *__restrict__ perm, uint64_t stride, uint32_t fixed_len,
-    uint64_t n, uint8_t *__restrict__ out, uint32_t dlen, int is384,
-    HKey<H::NW32> key, PadKW<typename H::word> pad, BurstArgs rx)
+/*
+ * One datagram / packet of hmac_kernel: binned position g (live: g < n).
+ * Shares the workgroup's key midstates (mid) and, for SHA-512, its LDS
+ * constant table; calls block_pad512 (a workgroup barrier), so every
+ * thread of the workgroup calls it the same number of times.
+ */
+template <class H, bool PADCONST, int MODE>
+__device__ __forceinline__ void hmac_item(uint64_t g,
+    const uint8_t *__restrict__ base, const uint64_t *__restrict__ offsets,
+    const uint32_t *__restrict__ lens, const uint32_t *__restrict__ perm,
+    uint64_t stride, uint32_t fixed_len, uint64_t n,
+    uint8_t *__restrict__ out, uint32_t dlen, int is384,
+    const PadKW<typename H::word> &pad, const BurstArgs &rx,
+    const uint32_t (*mid)[16])
 {
-	constexpr int NW32 = H::NW32;
-	/* [0..1]: the key's ipad / opad midstates; [2..3]: the alternate rx
-	 * key's (HMAC_BURST_RX with rx.alt) */
-	__shared__ uint32_t mid[4][16];
-	if (sizeof(typename H::word) == 8) {
-		if (PADCONST)
-			k512_lds_fill_pad(pad);
-		else
-			k512_lds_fill();
-	}
-	if (threadIdx.x < 64) {
-		/* lane 0: K' ^ ipad, lane 1: K' ^ opad, lanes 2 / 3 the same for
-		 * the alternate key -- one compression */
-		const int pass = threadIdx.x & 1;
-		const bool alt = MODE == HMAC_BURST_RX && (threadIdx.x & 2) != 0;
-		const uint32_t pad = pass ? 0x5c5c5c5cu : 0x36363636u;
-		typename H::State ks;
-		H::init(ks, is384);
-		uint32_t w[NW32];
-#pragma unroll
-		for (int i = 0; i < NW32; i++)
-			w[i] = (alt ? rx.altkey[i] : key.w[i]) ^ pad;
-		H::compress(ks, w);
-		materialize<H>(ks);
-		uint32_t kw[NW32];
-		digest_words<H>(ks, 0, kw);
-		if (threadIdx.x < (MODE == HMAC_BURST_RX && rx.alt ? 4u : 2u))
-#pragma unroll
-			for (int i = 0; i < 16; i++)
-				mid[threadIdx.x][i] = i < (sizeof(typename H::word) == 4 ? 8 : 16) ? kw[i] : 0u;
-	}
-	__syncthreads();
 	const uint32_t (*lmid)[16] = mid;	/* this lane's key */
-
-	const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	const bool live = g < n;
 	uint64_t i = g;
 	const uint8_t *p;
@@ -1357,6 +1386,59 @@ __attribute__((amdgpu_waves_per_eu(HmacWaves<H, MODE>::value))) void hmac_kernel
 		store_digest<32>(dst, o);
 	else
 		store_digest<64>(dst, o);
+}
+
+template <class H, bool PADCONST, int MODE = HMAC_DIGESTS>
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(HmacWaves<H, MODE>::value))) void hmac_kernel(const uint8_t *__restrict__ base,
+    const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
+    const uint32_t *__restrict__ perm, uint64_t stride, uint32_t fixed_len,
+    uint64_t n, uint8_t *__restrict__ out, uint32_t dlen, int is384,
+    HKey<H::NW32> key, PadKW<typename H::word> pad, BurstArgs rx,
+    const uint32_t *__restrict__ split)
+{
+	constexpr int NW32 = H::NW32;
+	/* [0..1]: the key's ipad / opad midstates; [2..3]: the alternate rx
+	 * key's (HMAC_BURST_RX with rx.alt) */
+	__shared__ uint32_t mid[4][16];
+	const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	uint64_t g2 = 0;
+	const int reps = short2_reps<H>(split, perm, n, g, g2);
+	if (reps == 0)
+		return;		/* the whole workgroup: lanes below take its packets */
+	if (sizeof(typename H::word) == 8) {
+		if (PADCONST)
+			k512_lds_fill_pad(pad);
+		else
+			k512_lds_fill();
+	}
+	if (threadIdx.x < 64) {
+		/* lane 0: K' ^ ipad, lane 1: K' ^ opad, lanes 2 / 3 the same for
+		 * the alternate key -- one compression */
+		const int pass = threadIdx.x & 1;
+		const bool alt = MODE == HMAC_BURST_RX && (threadIdx.x & 2) != 0;
+		const uint32_t pad = pass ? 0x5c5c5c5cu : 0x36363636u;
+		typename H::State ks;
+		H::init(ks, is384);
+		uint32_t w[NW32];
+#pragma unroll
+		for (int i = 0; i < NW32; i++)
+			w[i] = (alt ? rx.altkey[i] : key.w[i]) ^ pad;
+		H::compress(ks, w);
+		materialize<H>(ks);
+		uint32_t kw[NW32];
+		digest_words<H>(ks, 0, kw);
+		if (threadIdx.x < (MODE == HMAC_BURST_RX && rx.alt ? 4u : 2u))
+#pragma unroll
+			for (int i = 0; i < 16; i++)
+				mid[threadIdx.x][i] = i < (sizeof(typename H::word) == 4 ? 8 : 16) ? kw[i] : 0u;
+	}
+	__syncthreads();
+	hmac_item<H, PADCONST, MODE>(g, base, offsets, lens, perm, stride,
+	    fixed_len, n, out, dlen, is384, pad, rx, mid);
+	if (Short2<H>::value && reps == 2)
+		hmac_item<H, PADCONST, MODE>(g2, base, offsets, lens, perm, stride,
+		    fixed_len, n, out, dlen, is384, pad, rx, mid);
 }
 
 /* ---- coalesced small jobs (sha2_coalesce.cpp) ------------------------------- */
@@ -2025,8 +2107,10 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(
 struct BinHdr {
 	uint64_t magic;
 	uint32_t epoch, arrive, leave, state;
-	uint32_t pad[NET2_BIN_HDR - 6];
+	uint32_t split;		/* word NET2_BIN_SPLIT */
+	uint32_t pad[NET2_BIN_HDR - 7];
 };
+static_assert(offsetof(BinHdr, split) == 4 * NET2_BIN_SPLIT, "split word");
 static_assert(sizeof(BinHdr) == 4 * NET2_BIN_HDR, "header size");
 enum { BIN_UNDECIDED = 0, BIN_GO = 1, BIN_ABORT = 2 };
 
@@ -2072,6 +2156,8 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 	if (!bc[0]) {
 		/* not initialised: submission order now, initialise for next */
 		bin_identity(perm, n, ntiles);
+		if (blockIdx.x == 0 && threadIdx.x == 0)
+			h->split = (uint32_t)n;
 		if (blockIdx.x == 0) {
 			for (uint32_t w = threadIdx.x; w < 4 * NET2_SHA2_NBINS;
 			    w += blockDim.x)
@@ -2176,6 +2262,9 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		for (int j = 0; j < PER; j++)
 			pre[threadIdx.x * PER + j] = base + v[j];
 		__syncthreads();
+		/* where the packets of at most two blocks start (NET2_SHORT2) */
+		if (blockIdx.x == 0 && threadIdx.x == 0)
+			h->split = pre[NET2_SHA2_NBINS - 3];
 		for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
 			if (cnt[b] != 0)
 				cnt[b] = pre[b] + __hip_atomic_fetch_add(&cursor[b],
@@ -2198,9 +2287,11 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		}
 	} else {
 		bin_identity(perm, n, ntiles);
-		if (threadIdx.x == 0)	/* re-initialise at the next launch */
+		if (threadIdx.x == 0) {	/* re-initialise at the next launch */
 			__hip_atomic_store(&h->magic, 0ull, __ATOMIC_RELAXED,
 			    __HIP_MEMORY_SCOPE_AGENT);
+			h->split = (uint32_t)n;
+		}
 	}
 
 	/* the last workgroup out resets the barrier for the next launch */
@@ -2477,19 +2568,21 @@ hipError_t net2_launch_var(int alg, const uint8_t *base,
 	const int is384 = alg == NET2_ALG_SHA384;
 	const uint32_t dlen = s256 ? 32 : is384 ? 48 : 64;
 	uint32_t *perm = nullptr;
+	const uint32_t *split = nullptr;
 
 	if (ws != nullptr) {
 		hipError_t e = net2_bin_order(alg, lens, n, ws, s);
 		if (e != hipSuccess)
 			return e;
 		perm = ws + NET2_BIN_WS_WORDS;
+		split = ws + NET2_BIN_SPLIT;
 	}
 	if (s256)
 		var_kernel<Sha256V><<<grid_for(n), 256, 0, s>>>(base, offsets,
-		    lens, perm, n, out, dlen, 0);
+		    lens, perm, n, out, dlen, 0, split);
 	else
 		var_kernel<Sha512V><<<grid_for(n), 256, 0, s>>>(base, offsets,
-		    lens, perm, n, out, dlen, is384);
+		    lens, perm, n, out, dlen, is384, split);
 	return hipGetLastError();
 }
 /* H without the pair loop: the VERIFY kernel measured 1.5 % faster without
@@ -2504,25 +2597,26 @@ template <class H>
 static void launch_hmac_var_mode(int mode, unsigned grid, hipStream_t s,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
     const uint32_t *perm, uint64_t n, uint8_t *out, uint32_t dlen, int is384,
-    HKey<H::NW32> k, PadKW<typename H::word> pad, BurstArgs rx)
+    HKey<H::NW32> k, PadKW<typename H::word> pad, BurstArgs rx,
+    const uint32_t *split)
 {
 	if (mode == HMAC_SIGN)
 		hmac_kernel<H, false, HMAC_SIGN><<<grid, 256, 0, s>>>(base, offsets,
-		    lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx);
+		    lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx, split);
 	else if (mode == HMAC_VERIFY)
 		hmac_kernel<typename NoPair<H>::type, false, HMAC_VERIFY>
 		    <<<grid, 256, 0, s>>>(base, offsets, lens, perm, 0, 0, n, out,
-		    dlen, is384, k, pad, rx);
+		    dlen, is384, k, pad, rx, split);
 	else if (mode == HMAC_BURST_RX)
 		hmac_kernel<typename NoPair<H>::type, false, HMAC_BURST_RX>
 		    <<<grid, 256, 0, s>>>(base, offsets, lens, perm, 0, 0, n, out,
-		    dlen, is384, k, pad, rx);
+		    dlen, is384, k, pad, rx, split);
 	else if (mode == HMAC_BURST_TX)
 		hmac_kernel<H, false, HMAC_BURST_TX><<<grid, 256, 0, s>>>(base,
-		    offsets, lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx);
+		    offsets, lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx, split);
 	else
 		hmac_kernel<H, false><<<grid, 256, 0, s>>>(base, offsets,
-		    lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx);
+		    lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx, split);
 }
 
 hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
@@ -2549,11 +2643,13 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 	for (size_t i = 0; i < keylen; i++)
 		kb[i] = key[i];
 	uint32_t *perm = nullptr;
+	const uint32_t *split = nullptr;
 	if (offsets != nullptr && ws != nullptr) {
 		hipError_t e = net2_bin_order(halg, lens, n, ws, s);
 		if (e != hipSuccess)
 			return e;
 		perm = ws + NET2_BIN_WS_WORDS;
+		split = ws + NET2_BIN_SPLIT;
 	}
 	const unsigned grid = grid_for(n);
 	const bool padconst = offsets == nullptr && fixed_len % blk == 0;
@@ -2567,13 +2663,13 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 		if (padconst) {
 			pad_kw256(ibits, pad);
 			hmac_kernel<Sha256H, true><<<grid, 256, 0, s>>>(base, offsets,
-			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad, rx);
+			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad, rx, split);
 		} else if (offsets != nullptr) {
 			launch_hmac_var_mode<Sha256H>(mode, grid, s, base, offsets,
-			    lens, perm, n, out, dlen, 0, k, pad, rx);
+			    lens, perm, n, out, dlen, 0, k, pad, rx, split);
 		} else {
 			hmac_kernel<Sha256H, false><<<grid, 256, 0, s>>>(base, offsets,
-			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad, rx);
+			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad, rx, split);
 		}
 	} else {
 		HKey<32> k;
@@ -2584,13 +2680,13 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 		if (padconst) {
 			pad_kw512(ibits, pad);
 			hmac_kernel<Sha512HF, true><<<grid, 256, 0, s>>>(base, offsets,
-			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad, rx);
+			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad, rx, split);
 		} else if (offsets != nullptr) {
 			launch_hmac_var_mode<Sha512H>(mode, grid, s, base, offsets,
-			    lens, perm, n, out, dlen, is384, k, pad, rx);
+			    lens, perm, n, out, dlen, is384, k, pad, rx, split);
 		} else {
 			hmac_kernel<Sha512HF, false><<<grid, 256, 0, s>>>(base, offsets,
-			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad, rx);
+			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad, rx, split);
 		}
 	}
 	return hipGetLastError();

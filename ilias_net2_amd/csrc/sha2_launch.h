@@ -26,6 +26,9 @@
  */
 #define NET2_BIN_HDR 16
 #define NET2_BIN_WS_WORDS (NET2_BIN_HDR + 4 * NET2_SHA2_NBINS)
+/* header word: the binned order's first packet of at most two blocks (the
+ * short tail), or n when the order is not binned */
+#define NET2_BIN_SPLIT 6
 
 /* Fixed-stride batch; base/out in device memory, async on s. */
 hipError_t net2_launch_fixed(int alg, const uint8_t *base, uint64_t stride,
