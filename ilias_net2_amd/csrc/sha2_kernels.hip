@@ -2069,17 +2069,21 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(
  * One-pass binning (NET2_BIN_ONEPASS): the count, the global prefix and the
  * scatter in one launch, no memset.  A persistent grid of G <= 256
  * workgroups (each loops over its 4,096-packet tiles):
- *   1. LDS histogram of its tiles, added to the global histogram (one
- *      device-scope atomic per touched bin);
+ *   1. LDS histogram of its tiles, each packet's rank in its bin kept in
+ *      registers (the LDS atomic's return value), then one device-scope
+ *      fetch-add per touched bin into the global histogram, whose old value
+ *      is where the workgroup's packets start inside that bin;
  *   2. a grid barrier on an arrival counter in the workspace header (the
- *      last arriver flips `state` to GO);
+ *      last arriver flips `state` to GO; the others poll it relaxed and
+ *      take one acquire fence when it is decided);
  *   3. every workgroup scans the global histogram (8 KiB) for the bin
- *      bases, claims its ranges (one atomic per touched bin) and writes
- *      perm from LDS ranks -- as bin_scatter_kernel, minus its launch.
- * The workspace cleans up after itself: the histogram and claim counters
- * come in two parities, each launch zeroes the one the next launch uses
- * (the header's epoch selects), and the last workgroup to leave resets the
- * counters and bumps the epoch.
+ *      bases and writes perm[base + start + rank] -- no claim pass, no
+ *      second read of the lengths (a workgroup with several tiles, above
+ *      256 x 4,096 packets, ranks them again from the same starts).
+ * The workspace cleans up after itself: the histogram comes in two
+ * parities, each launch zeroes the one the next launch uses (the header's
+ * epoch selects), and the last workgroup to leave resets the counters and
+ * bumps the epoch.
  *
  * Never a hang, never a wrong order:
  *   - a barrier that does not complete within NET2_BIN_TIMEOUT (the grid
@@ -2098,6 +2102,12 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(
  */
 #ifndef NET2_BIN_ONEPASS
 #define NET2_BIN_ONEPASS 1
+#endif
+#ifndef NET2_BIN_SPIN_ACQ
+#define NET2_BIN_SPIN_ACQ 0
+#endif
+#ifndef NET2_BIN_SPIN_SLEEP
+#define NET2_BIN_SPIN_SLEEP 2
 #endif
 #define NET2_BIN_MAGIC 0x4e45543242494e53ull	/* "NET2BINS" */
 #define NET2_BIN_GRID 256
@@ -2142,7 +2152,6 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 	__shared__ uint32_t bc[2];
 	BinHdr *h = reinterpret_cast<BinHdr *>(ws);
 	uint32_t *hist0 = ws + NET2_BIN_HDR;		/* [2][NBINS] */
-	uint32_t *cur0 = hist0 + 2 * NET2_SHA2_NBINS;	/* [2][NBINS] */
 	uint32_t *perm = ws + NET2_BIN_WS_WORDS;
 	const uint32_t G = gridDim.x;
 	const uint64_t ntiles = (n + NET2_BIN_TILE - 1) / NET2_BIN_TILE;
@@ -2178,34 +2187,42 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 	}
 	const uint32_t par = bc[1] & 1;
 	uint32_t *hist = hist0 + par * NET2_SHA2_NBINS;
-	uint32_t *cursor = cur0 + par * NET2_SHA2_NBINS;
 	/* the next launch's parity, zeroed across the grid */
 	for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-	    w < NET2_SHA2_NBINS; w += G * blockDim.x) {
+	    w < NET2_SHA2_NBINS; w += G * blockDim.x)
 		hist0[(par ^ 1) * NET2_SHA2_NBINS + w] = 0;
-		cur0[(par ^ 1) * NET2_SHA2_NBINS + w] = 0;
-	}
 
-	/* 1: this workgroup's histogram, into the global one */
+	/* 1: this workgroup's histogram; the LDS atomics' return values are the
+	 * ranks of its first tile's packets, kept in registers */
 	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
 		cnt[b] = 0;
 	__syncthreads();
+	uint32_t bin0[NET2_BIN_ITEMS], rank0[NET2_BIN_ITEMS];
 	for (uint64_t t = blockIdx.x; t < ntiles; t += G) {
 		const uint64_t i0 = t * NET2_BIN_TILE + threadIdx.x;
 		uint32_t len[NET2_BIN_ITEMS];
 		load_lens(lens, n, i0, len);
 #pragma unroll
-		for (int k = 0; k < NET2_BIN_ITEMS; k++)
-			if (i0 + (uint64_t)k * 256 < n)
-				atomicAdd(&cnt[bin_of(len[k], blk_shift, lenbytes,
-				    NET2_SHA2_NBINS)], 1u);
+		for (int k = 0; k < NET2_BIN_ITEMS; k++) {
+			const uint32_t bn = bin_of(len[k], blk_shift, lenbytes,
+			    NET2_SHA2_NBINS);
+			const uint32_t r = i0 + (uint64_t)k * 256 < n ?
+			    atomicAdd(&cnt[bn], 1u) : 0u;
+			if (t == blockIdx.x) {
+				bin0[k] = bn;
+				rank0[k] = r;
+			}
+		}
 	}
 	__syncthreads();
+	/* into the global histogram: the add's old value is where this
+	 * workgroup's packets start inside each bin (no claim pass) */
 	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
 		if (cnt[b] != 0)
-			__hip_atomic_fetch_add(&hist[b], cnt[b], __ATOMIC_RELAXED,
-			    __HIP_MEMORY_SCOPE_AGENT);
-	__threadfence();
+			cnt[b] = __hip_atomic_fetch_add(&hist[b], cnt[b],
+			    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	if (NET2_BIN_SPIN_ACQ)
+		__threadfence();
 	__syncthreads();
 
 	/* 2: grid barrier, decided GO or ABORT exactly once */
@@ -2220,23 +2237,28 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		}
 		const uint64_t t0 = wall_clock64();
 		uint32_t st;
-		while ((st = __hip_atomic_load(&h->state, __ATOMIC_ACQUIRE,
-		    __HIP_MEMORY_SCOPE_AGENT)) == BIN_UNDECIDED) {
+		/* relaxed polls, one acquire fence once decided
+		 * (NET2_BIN_SPIN_ACQ=1: an acquiring load per poll) */
+		while ((st = NET2_BIN_SPIN_ACQ ? __hip_atomic_load(&h->state,
+		    __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) :
+		    ld_agent(&h->state)) == BIN_UNDECIDED) {
 			if (wall_clock64() - t0 > timeout) {
 				uint32_t exp = BIN_UNDECIDED;
 				__hip_atomic_compare_exchange_strong(&h->state,
 				    &exp, (uint32_t)BIN_ABORT, __ATOMIC_ACQ_REL,
 				    __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
 			}
-			__builtin_amdgcn_s_sleep(8);
+			__builtin_amdgcn_s_sleep(NET2_BIN_SPIN_SLEEP);
 		}
+		if (!NET2_BIN_SPIN_ACQ)
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 		bc[0] = st;
 	}
 	__syncthreads();
 	if (bc[0] == BIN_GO) {
 		/* 3: bin bases from the global histogram (8 bins per thread, a
-		 * shuffle scan per wave, the four wave totals), this
-		 * workgroup's ranges, then its packets' places */
+		 * shuffle scan per wave, the four wave totals), then this
+		 * workgroup's packets' places */
 		constexpr int PER = NET2_SHA2_NBINS / 256;
 		const int lane = (int)__lane_id(), wave = (int)(threadIdx.x / 64);
 		uint32_t v[PER], sum = 0;
@@ -2265,23 +2287,38 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		/* where the packets of at most two blocks start (NET2_SHORT2) */
 		if (blockIdx.x == 0 && threadIdx.x == 0)
 			h->split = pre[NET2_SHA2_NBINS - 3];
-		for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
-			if (cnt[b] != 0)
-				cnt[b] = pre[b] + __hip_atomic_fetch_add(&cursor[b],
-				    cnt[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-		__syncthreads();
-		for (uint64_t t = blockIdx.x; t < ntiles; t += G) {
-			const uint64_t i0 = t * NET2_BIN_TILE + threadIdx.x;
-			uint32_t len[NET2_BIN_ITEMS];
-			load_lens(lens, n, i0, len);
+		if (ntiles <= G) {
+			/* one tile: its packets' places from the kept ranks */
+			const uint64_t i0 = (uint64_t)blockIdx.x * NET2_BIN_TILE +
+			    threadIdx.x;
 #pragma unroll
 			for (int k = 0; k < NET2_BIN_ITEMS; k++) {
 				const uint64_t i = i0 + (uint64_t)k * 256;
-				if (i < n) {
-					const uint32_t pos = atomicAdd(&cnt[bin_of(len[k],
-					    blk_shift, lenbytes, NET2_SHA2_NBINS)], 1u);
-					if (pos < n)
-						perm[pos] = (uint32_t)i;
+				const uint32_t pos = pre[bin0[k]] + cnt[bin0[k]] +
+				    rank0[k];
+				if (i < n && pos < n)
+					perm[pos] = (uint32_t)i;
+			}
+		} else {
+			/* several tiles: rank them again from the bin starts */
+			for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS;
+			    b += blockDim.x)
+				cnt[b] += pre[b];
+			__syncthreads();
+			for (uint64_t t = blockIdx.x; t < ntiles; t += G) {
+				const uint64_t i0 = t * NET2_BIN_TILE + threadIdx.x;
+				uint32_t len[NET2_BIN_ITEMS];
+				load_lens(lens, n, i0, len);
+#pragma unroll
+				for (int k = 0; k < NET2_BIN_ITEMS; k++) {
+					const uint64_t i = i0 + (uint64_t)k * 256;
+					if (i < n) {
+						const uint32_t pos = atomicAdd(
+						    &cnt[bin_of(len[k], blk_shift,
+						    lenbytes, NET2_SHA2_NBINS)], 1u);
+						if (pos < n)
+							perm[pos] = (uint32_t)i;
+					}
 				}
 			}
 		}
@@ -2294,8 +2331,11 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		}
 	}
 
-	/* the last workgroup out resets the barrier for the next launch */
-	__threadfence();
+	/* the last workgroup out resets the barrier for the next launch (the
+	 * leave counter's acq_rel orders this workgroup's reads of the header
+	 * before the reset; perm is published by the kernel's end) */
+	if (NET2_BIN_SPIN_ACQ)
+		__threadfence();
 	__syncthreads();
 	if (threadIdx.x == 0) {
 		const uint32_t old = __hip_atomic_fetch_add(&h->leave, 1u,
