@@ -2069,21 +2069,22 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(
  * One-pass binning (NET2_BIN_ONEPASS): the count, the global prefix and the
  * scatter in one launch, no memset.  A persistent grid of G <= 256
  * workgroups (each loops over its 4,096-packet tiles):
- *   1. LDS histogram of its tiles, each packet's rank in its bin kept in
- *      registers (the LDS atomic's return value), then one device-scope
- *      fetch-add per touched bin into the global histogram, whose old value
- *      is where the workgroup's packets start inside that bin;
- *   2. a grid barrier on an arrival counter in the workspace header (the
- *      last arriver flips `state` to GO; the others poll it relaxed and
- *      take one acquire fence when it is decided);
+ *   1. LDS histogram of its tiles (NET2_BIN_COPIES copies), each packet's
+ *      rank in its copy of its bin kept in registers (the LDS atomic's
+ *      return value), then one device-scope fetch-add per touched bin into
+ *      the global histogram, whose old value is where the workgroup's
+ *      packets start inside that bin;
+ *   2. a grid barrier in two levels: 16 group counters (workgroup
+ *      blockIdx & 15, one XCD each), the last of each group arrives at a top
+ *      counter, the last of those flips `state` to GO and bumps the epoch;
+ *      everyone polls `state`;
  *   3. every workgroup scans the global histogram (8 KiB) for the bin
  *      bases and writes perm[base + start + rank] -- no claim pass, no
  *      second read of the lengths (a workgroup with several tiles, above
  *      256 x 4,096 packets, ranks them again from the same starts).
- * The workspace cleans up after itself: the histogram comes in two
- * parities, each launch zeroes the one the next launch uses (the header's
- * epoch selects), and the last workgroup to leave resets the counters and
- * bumps the epoch.
+ * The workspace cleans up after itself: the histogram and the barrier words
+ * come in two parities (the epoch selects); each launch zeroes the parity
+ * the next launch uses, so nothing waits for the last workgroup to leave.
  *
  * Never a hang, never a wrong order:
  *   - a barrier that does not complete within NET2_BIN_TIMEOUT (the grid
@@ -2099,16 +2100,53 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(
  *   - the hash kernels clamp perm entries to [0, n) (a corrupt workspace
  *     can cost digests, never an out-of-bounds access).
  * The workspace must not be used by two launches at once (as before).
+ *
+ * Memory ordering.  What crosses the barrier is the histogram, written and
+ * read only by device-scope atomics, each workgroup's adds returned before
+ * it arrives; the plain stores (perm, the next parity's zeroes) are read
+ * only by later launches.  So the barrier needs no cache maintenance
+ * (NET2_BIN_FENCE=0, shipped).  On gfx950 an agent-scope release writes back
+ * the XCD's L2 and an acquire invalidates it; with acq_rel arrivals and an
+ * acquire fence (1) the launch measured ~15 % longer, with an acquiring
+ * load per poll (2) ~3x (profiles/round4/bin_probe_*.txt).
  */
 #ifndef NET2_BIN_ONEPASS
 #define NET2_BIN_ONEPASS 1
 #endif
-#ifndef NET2_BIN_SPIN_ACQ
-#define NET2_BIN_SPIN_ACQ 0
+#ifndef NET2_BIN_FENCE
+#define NET2_BIN_FENCE 0
 #endif
+#define BIN_ORD (NET2_BIN_FENCE >= 1 ? __ATOMIC_ACQ_REL : __ATOMIC_RELAXED)
+#define BIN_ACQ (NET2_BIN_FENCE >= 1 ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED)
 #ifndef NET2_BIN_SPIN_SLEEP
 #define NET2_BIN_SPIN_SLEEP 2
 #endif
+/*
+ * LDS histogram copies (power of two): lane l counts into copy l & (C-1), so
+ * a wave's atomics on one bin spread over C addresses -- the LDS serialises
+ * equal addresses, and a batch of few lengths (the C3 mix: 3) puts ~21
+ * lanes of every wave on each.  A packet's rank in its bin is then the
+ * copies before its own plus its rank in that copy.
+ */
+#ifndef NET2_BIN_COPIES
+#define NET2_BIN_COPIES 8
+#endif
+#define NET2_BIN_GROUPS 16
+/*
+ * Barrier words, per parity, in the workspace after the two histograms
+ * (each on its own 128-byte line): group counters at 32 g, the top counter
+ * at 512, the state at 544.  Words 2,048-4,095 of the area hold the probe
+ * stamps (NET2_BIN_PROBE=1, tools/bin_probe.py: thread 0 of every
+ * workgroup stamps the 100 MHz clock at eight points).
+ */
+#define BIN_CTL_PAR 1024
+#define BIN_CTL_TOP 512
+#define BIN_CTL_STATE 544
+#ifndef NET2_BIN_PROBE
+#define NET2_BIN_PROBE 0
+#endif
+#define BIN_STAMP(p) do { if (NET2_BIN_PROBE && threadIdx.x == 0) \
+	ctl0[2048 + blockIdx.x * 8 + (p)] = (uint32_t)wall_clock64(); } while (0)
 #define NET2_BIN_MAGIC 0x4e45543242494e53ull	/* "NET2BINS" */
 #define NET2_BIN_GRID 256
 /* 50 ms of the 100 MHz s_memrealtime clock */
@@ -2116,12 +2154,15 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(
 
 struct BinHdr {
 	uint64_t magic;
-	uint32_t epoch, arrive, leave, state;
+	uint32_t epoch, rsv[3];
 	uint32_t split;		/* word NET2_BIN_SPLIT */
 	uint32_t pad[NET2_BIN_HDR - 7];
 };
 static_assert(offsetof(BinHdr, split) == 4 * NET2_BIN_SPLIT, "split word");
 static_assert(sizeof(BinHdr) == 4 * NET2_BIN_HDR, "header size");
+static_assert(2048 + NET2_BIN_GRID * 8 <= 2 * NET2_SHA2_NBINS, "probe words");
+static_assert(BIN_CTL_STATE < BIN_CTL_PAR && 32 * NET2_BIN_GROUPS <= BIN_CTL_TOP,
+    "barrier words");
 enum { BIN_UNDECIDED = 0, BIN_GO = 1, BIN_ABORT = 2 };
 
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t *p)
@@ -2146,21 +2187,29 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
     const uint32_t *__restrict__ lens, uint64_t n, int blk_shift,
     int lenbytes, uint32_t *__restrict__ ws, uint64_t timeout)
 {
-	__shared__ uint32_t cnt[NET2_SHA2_NBINS];
-	__shared__ uint32_t pre[NET2_SHA2_NBINS];
+	__shared__ uint32_t cnt[NET2_BIN_COPIES * NET2_SHA2_NBINS];
+	__shared__ uint32_t start[NET2_SHA2_NBINS];
 	__shared__ uint32_t wsum[4];
 	__shared__ uint32_t bc[2];
 	BinHdr *h = reinterpret_cast<BinHdr *>(ws);
-	uint32_t *hist0 = ws + NET2_BIN_HDR;		/* [2][NBINS] */
+	uint32_t *hist0 = ws + NET2_BIN_HDR;			/* [2][NBINS] */
+	uint32_t *ctl0 = hist0 + 2 * NET2_SHA2_NBINS;		/* [2][1024] */
 	uint32_t *perm = ws + NET2_BIN_WS_WORDS;
 	const uint32_t G = gridDim.x;
 	const uint64_t ntiles = (n + NET2_BIN_TILE - 1) / NET2_BIN_TILE;
 
+	/* the first tile's lengths in flight while the header is read */
+	uint32_t len[NET2_BIN_ITEMS];
+	load_lens(lens, n, (uint64_t)blockIdx.x * NET2_BIN_TILE + threadIdx.x,
+	    len);
 	if (threadIdx.x == 0) {
-		bc[0] = __hip_atomic_load(&h->magic, __ATOMIC_ACQUIRE,
+		bc[0] = __hip_atomic_load(&h->magic, BIN_ACQ,
 		    __HIP_MEMORY_SCOPE_AGENT) == NET2_BIN_MAGIC;
 		bc[1] = ld_agent(&h->epoch);
 	}
+	for (uint32_t b = threadIdx.x; b < NET2_BIN_COPIES * NET2_SHA2_NBINS / 4;
+	    b += blockDim.x)
+		reinterpret_cast<uint4 *>(cnt)[b] = make_uint4(0, 0, 0, 0);
 	__syncthreads();
 	if (!bc[0]) {
 		/* not initialised: submission order now, initialise for next */
@@ -2168,15 +2217,11 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		if (blockIdx.x == 0 && threadIdx.x == 0)
 			h->split = (uint32_t)n;
 		if (blockIdx.x == 0) {
-			for (uint32_t w = threadIdx.x; w < 4 * NET2_SHA2_NBINS;
-			    w += blockDim.x)
+			for (uint32_t w = threadIdx.x; w < 2 * NET2_SHA2_NBINS +
+			    2 * BIN_CTL_PAR; w += blockDim.x)
 				hist0[w] = 0;
-			if (threadIdx.x == 0) {
+			if (threadIdx.x == 0)
 				h->epoch = 0;
-				h->arrive = 0;
-				h->leave = 0;
-				h->state = BIN_UNDECIDED;
-			}
 			__threadfence();
 			__syncthreads();
 			if (threadIdx.x == 0)
@@ -2185,29 +2230,36 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		}
 		return;
 	}
+	BIN_STAMP(0);
 	const uint32_t par = bc[1] & 1;
 	uint32_t *hist = hist0 + par * NET2_SHA2_NBINS;
-	/* the next launch's parity, zeroed across the grid */
+	uint32_t *ctl = ctl0 + par * BIN_CTL_PAR;
+	/* the next launch's parity, zeroed: its histogram across the grid, its
+	 * barrier words by workgroup 0 */
 	for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
 	    w < NET2_SHA2_NBINS; w += G * blockDim.x)
 		hist0[(par ^ 1) * NET2_SHA2_NBINS + w] = 0;
+	if (blockIdx.x == 0 && threadIdx.x <= NET2_BIN_GROUPS + 1) {
+		const uint32_t w = threadIdx.x < NET2_BIN_GROUPS ? 32 * threadIdx.x :
+		    threadIdx.x == NET2_BIN_GROUPS ? BIN_CTL_TOP : BIN_CTL_STATE;
+		ctl0[(par ^ 1) * BIN_CTL_PAR + w] = 0;
+	}
 
-	/* 1: this workgroup's histogram; the LDS atomics' return values are the
-	 * ranks of its first tile's packets, kept in registers */
-	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
-		cnt[b] = 0;
-	__syncthreads();
+	/* 1: this workgroup's histogram (in this lane's copy); the ranks of its
+	 * first tile's packets kept in registers */
+	uint32_t *mine = cnt + (__lane_id() & (NET2_BIN_COPIES - 1)) *
+	    NET2_SHA2_NBINS;
 	uint32_t bin0[NET2_BIN_ITEMS], rank0[NET2_BIN_ITEMS];
 	for (uint64_t t = blockIdx.x; t < ntiles; t += G) {
 		const uint64_t i0 = t * NET2_BIN_TILE + threadIdx.x;
-		uint32_t len[NET2_BIN_ITEMS];
-		load_lens(lens, n, i0, len);
+		if (t != blockIdx.x)
+			load_lens(lens, n, i0, len);
 #pragma unroll
 		for (int k = 0; k < NET2_BIN_ITEMS; k++) {
 			const uint32_t bn = bin_of(len[k], blk_shift, lenbytes,
 			    NET2_SHA2_NBINS);
 			const uint32_t r = i0 + (uint64_t)k * 256 < n ?
-			    atomicAdd(&cnt[bn], 1u) : 0u;
+			    atomicAdd(&mine[bn], 1u) : 0u;
 			if (t == blockIdx.x) {
 				bin0[k] = bn;
 				rank0[k] = r;
@@ -2215,50 +2267,65 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		}
 	}
 	__syncthreads();
-	/* into the global histogram: the add's old value is where this
-	 * workgroup's packets start inside each bin (no claim pass) */
-	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
-		if (cnt[b] != 0)
-			cnt[b] = __hip_atomic_fetch_add(&hist[b], cnt[b],
-			    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-	if (NET2_BIN_SPIN_ACQ)
-		__threadfence();
+	BIN_STAMP(1);
+	/* copies -> their exclusive prefix per bin; the bin's total into the
+	 * global histogram, whose old value is where this workgroup's packets
+	 * start inside the bin */
+	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x) {
+		uint32_t acc = 0;
+#pragma unroll
+		for (int c = 0; c < NET2_BIN_COPIES; c++) {
+			const uint32_t v = cnt[c * NET2_SHA2_NBINS + b];
+			cnt[c * NET2_SHA2_NBINS + b] = acc;
+			acc += v;
+		}
+		start[b] = acc != 0 ? __hip_atomic_fetch_add(&hist[b], acc,
+		    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+	}
 	__syncthreads();
+	BIN_STAMP(2);
 
-	/* 2: grid barrier, decided GO or ABORT exactly once */
+	/* 2: grid barrier in two levels, decided GO or ABORT exactly once */
 	if (threadIdx.x == 0) {
-		const uint32_t old = __hip_atomic_fetch_add(&h->arrive, 1u,
-		    __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-		if (old == G - 1) {
+		const uint32_t ng = G < NET2_BIN_GROUPS ? G : NET2_BIN_GROUPS;
+		const uint32_t g = blockIdx.x % NET2_BIN_GROUPS;
+		const uint32_t gsize = (G - g + NET2_BIN_GROUPS - 1) /
+		    NET2_BIN_GROUPS;
+		if (__hip_atomic_fetch_add(&ctl[32 * g], 1u, BIN_ORD,
+		    __HIP_MEMORY_SCOPE_AGENT) == gsize - 1 &&
+		    __hip_atomic_fetch_add(&ctl[BIN_CTL_TOP], 1u, BIN_ORD,
+		    __HIP_MEMORY_SCOPE_AGENT) == ng - 1) {
+			/* every workgroup has read the epoch by now */
+			__hip_atomic_store(&h->epoch, bc[1] + 1, __ATOMIC_RELAXED,
+			    __HIP_MEMORY_SCOPE_AGENT);
 			uint32_t exp = BIN_UNDECIDED;
-			__hip_atomic_compare_exchange_strong(&h->state, &exp,
-			    (uint32_t)BIN_GO, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+			__hip_atomic_compare_exchange_strong(&ctl[BIN_CTL_STATE],
+			    &exp, (uint32_t)BIN_GO, BIN_ORD, BIN_ACQ,
 			    __HIP_MEMORY_SCOPE_AGENT);
 		}
+		BIN_STAMP(3);
 		const uint64_t t0 = wall_clock64();
 		uint32_t st;
-		/* relaxed polls, one acquire fence once decided
-		 * (NET2_BIN_SPIN_ACQ=1: an acquiring load per poll) */
-		while ((st = NET2_BIN_SPIN_ACQ ? __hip_atomic_load(&h->state,
-		    __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) :
-		    ld_agent(&h->state)) == BIN_UNDECIDED) {
+		while ((st = ld_agent(&ctl[BIN_CTL_STATE])) == BIN_UNDECIDED) {
 			if (wall_clock64() - t0 > timeout) {
 				uint32_t exp = BIN_UNDECIDED;
-				__hip_atomic_compare_exchange_strong(&h->state,
-				    &exp, (uint32_t)BIN_ABORT, __ATOMIC_ACQ_REL,
-				    __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+				__hip_atomic_compare_exchange_strong(
+				    &ctl[BIN_CTL_STATE], &exp,
+				    (uint32_t)BIN_ABORT, BIN_ORD, BIN_ACQ,
+				    __HIP_MEMORY_SCOPE_AGENT);
 			}
 			__builtin_amdgcn_s_sleep(NET2_BIN_SPIN_SLEEP);
 		}
-		if (!NET2_BIN_SPIN_ACQ)
+		if (NET2_BIN_FENCE >= 1)
 			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+		BIN_STAMP(4);
 		bc[0] = st;
 	}
 	__syncthreads();
 	if (bc[0] == BIN_GO) {
 		/* 3: bin bases from the global histogram (8 bins per thread, a
-		 * shuffle scan per wave, the four wave totals), then this
-		 * workgroup's packets' places */
+		 * shuffle scan per wave, the four wave totals) added to the
+		 * workgroup's starts, then its packets' places */
 		constexpr int PER = NET2_SHA2_NBINS / 256;
 		const int lane = (int)__lane_id(), wave = (int)(threadIdx.x / 64);
 		uint32_t v[PER], sum = 0;
@@ -2281,12 +2348,16 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		for (int w = 0; w < wave; w++)
 			base += wsum[w];
 #pragma unroll
-		for (int j = 0; j < PER; j++)
-			pre[threadIdx.x * PER + j] = base + v[j];
+		for (int j = 0; j < PER; j++) {
+			const uint32_t b = threadIdx.x * PER + j;
+			start[b] += base + v[j];
+			/* where the packets of at most two blocks start
+			 * (NET2_SHORT2) */
+			if (blockIdx.x == 0 && b == NET2_SHA2_NBINS - 3)
+				h->split = base + v[j];
+		}
 		__syncthreads();
-		/* where the packets of at most two blocks start (NET2_SHORT2) */
-		if (blockIdx.x == 0 && threadIdx.x == 0)
-			h->split = pre[NET2_SHA2_NBINS - 3];
+		BIN_STAMP(5);
 		if (ntiles <= G) {
 			/* one tile: its packets' places from the kept ranks */
 			const uint64_t i0 = (uint64_t)blockIdx.x * NET2_BIN_TILE +
@@ -2294,20 +2365,20 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 #pragma unroll
 			for (int k = 0; k < NET2_BIN_ITEMS; k++) {
 				const uint64_t i = i0 + (uint64_t)k * 256;
-				const uint32_t pos = pre[bin0[k]] + cnt[bin0[k]] +
-				    rank0[k];
+				const uint32_t pos = start[bin0[k]] +
+				    mine[bin0[k]] + rank0[k];
 				if (i < n && pos < n)
 					perm[pos] = (uint32_t)i;
 			}
 		} else {
-			/* several tiles: rank them again from the bin starts */
+			/* several tiles: rank them again from the starts, one
+			 * counter per bin */
 			for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS;
 			    b += blockDim.x)
-				cnt[b] += pre[b];
+				cnt[b] = start[b];
 			__syncthreads();
 			for (uint64_t t = blockIdx.x; t < ntiles; t += G) {
 				const uint64_t i0 = t * NET2_BIN_TILE + threadIdx.x;
-				uint32_t len[NET2_BIN_ITEMS];
 				load_lens(lens, n, i0, len);
 #pragma unroll
 				for (int k = 0; k < NET2_BIN_ITEMS; k++) {
@@ -2322,6 +2393,7 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 				}
 			}
 		}
+		BIN_STAMP(6);
 	} else {
 		bin_identity(perm, n, ntiles);
 		if (threadIdx.x == 0) {	/* re-initialise at the next launch */
@@ -2330,38 +2402,17 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 			h->split = (uint32_t)n;
 		}
 	}
-
-	/* the last workgroup out resets the barrier for the next launch (the
-	 * leave counter's acq_rel orders this workgroup's reads of the header
-	 * before the reset; perm is published by the kernel's end) */
-	if (NET2_BIN_SPIN_ACQ)
-		__threadfence();
-	__syncthreads();
-	if (threadIdx.x == 0) {
-		const uint32_t old = __hip_atomic_fetch_add(&h->leave, 1u,
-		    __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-		if (old == G - 1) {
-			h->arrive = 0;
-			h->leave = 0;
-			h->state = BIN_UNDECIDED;
-			h->epoch = bc[1] + 1;
-			__threadfence();
-		}
-	}
 }
 
 /* Prepares a binning workspace so its first launch bins (one workgroup). */
 __global__ __launch_bounds__(256) void bin_ws_init_kernel(uint32_t *ws)
 {
 	BinHdr *h = reinterpret_cast<BinHdr *>(ws);
-	for (uint32_t w = threadIdx.x; w < 4 * NET2_SHA2_NBINS; w += blockDim.x)
+	for (uint32_t w = threadIdx.x; w < 2 * NET2_SHA2_NBINS + 2 * BIN_CTL_PAR;
+	    w += blockDim.x)
 		ws[NET2_BIN_HDR + w] = 0;
-	if (threadIdx.x == 0) {
+	if (threadIdx.x == 0)
 		h->epoch = 0;
-		h->arrive = 0;
-		h->leave = 0;
-		h->state = BIN_UNDECIDED;
-	}
 	__threadfence();
 	__syncthreads();
 	if (threadIdx.x == 0)

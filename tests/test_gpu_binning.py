@@ -68,10 +68,17 @@ def test_workspace_lifecycle(dev, oracle_mod, alg):
             assert np.array_equal(order, np.arange(n))
         else:
             assert (np.diff(bl[order]) <= 0).all(), call
-    # epoch counts the binned launches (header word 2), arrive / leave /
-    # state back to zero between launches
-    hdr = ws.cpu().numpy()[:6].view(np.uint32)
-    assert hdr[2] == 5 and hdr[3] == 0 and hdr[4] == 0 and hdr[5] == 0, hdr
+    # epoch counts the binned launches (header word 2); the barrier words
+    # (after the two histograms, 1,024 per parity: group counters every 32
+    # words, top counter at 512, state at 544) -- the last launch's parity
+    # (0) decided GO with every workgroup arrived, the next one's zeroed
+    w = ws.cpu().numpy().view(np.uint32)
+    assert w[2] == 5, w[:8]
+    ctl = w[16 + 2 * 2048:16 + 2 * 2048 + 2 * 1024].reshape(2, 1024)
+    G = min(256, (n + 4095) // 4096)
+    assert ctl[0, 544] == 1 and ctl[0, 512] == min(G, 16), ctl[0, [512, 544]]
+    assert ctl[0, 0:512:32].sum() == G
+    assert not ctl[1, 0:512:32].any() and ctl[1, 512] == 0 and ctl[1, 544] == 0
 
 
 def test_prepared_workspace_bins_from_the_first_call(dev, oracle_mod):
