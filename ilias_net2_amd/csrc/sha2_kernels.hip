@@ -2069,11 +2069,11 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(
  * One-pass binning (NET2_BIN_ONEPASS): the count, the global prefix and the
  * scatter in one launch, no memset.  A persistent grid of G <= 256
  * workgroups (each loops over its 4,096-packet tiles):
- *   1. LDS histogram of its tiles (NET2_BIN_COPIES copies), each packet's
- *      rank in its copy of its bin kept in registers (the LDS atomic's
- *      return value), then one device-scope fetch-add per touched bin into
- *      the global histogram, whose old value is where the workgroup's
- *      packets start inside that bin;
+ *   1. LDS histogram of its tiles, each packet's rank in its bin kept in
+ *      registers (the LDS atomic's return value), then one device-scope
+ *      fetch-add per touched bin into the global histogram (its slice of
+ *      it), whose old value is where the workgroup's packets start inside
+ *      that bin, after the slices before its own;
  *   2. a grid barrier in two levels: 16 group counters (workgroup
  *      blockIdx & 15, one XCD each), the last of each group arrives at a top
  *      counter, the last of those flips `state` to GO and bumps the epoch;
@@ -2122,19 +2122,20 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(
 #define NET2_BIN_SPIN_SLEEP 2
 #endif
 /*
- * LDS histogram copies (power of two): lane l counts into copy l & (C-1), so
- * a wave's atomics on one bin spread over C addresses -- the LDS serialises
- * equal addresses, and a batch of few lengths (the C3 mix: 3) puts ~21
- * lanes of every wave on each.  A packet's rank in its bin is then the
- * copies before its own plus its rank in that copy.
+ * Global histogram slices (power of two, <= 8): workgroup w adds into slice
+ * w & (S-1) (its XCD), so each bin's device-scope adds queue on S addresses
+ * instead of one; a workgroup's start inside a bin is then the slices
+ * before its own plus its add's old value in its slice.
  */
-#ifndef NET2_BIN_COPIES
-#define NET2_BIN_COPIES 8
+#ifndef NET2_BIN_SLICES
+#define NET2_BIN_SLICES 8
 #endif
+static_assert(NET2_BIN_SLICES >= 1 && NET2_BIN_SLICES <= 8 &&
+    (NET2_BIN_SLICES & (NET2_BIN_SLICES - 1)) == 0, "slices");
 #define NET2_BIN_GROUPS 16
 /*
- * Barrier words, per parity, in the workspace after the two histograms
- * (each on its own 128-byte line): group counters at 32 g, the top counter
+ * Barrier words, per parity, in the workspace after the histograms (two
+ * parities of up to eight slices; each word on its own 128-byte line): group counters at 32 g, the top counter
  * at 512, the state at 544.  Words 2,048-4,095 of the area hold the probe
  * stamps (NET2_BIN_PROBE=1, tools/bin_probe.py: thread 0 of every
  * workgroup stamps the 100 MHz clock at eight points).
@@ -2160,7 +2161,10 @@ struct BinHdr {
 };
 static_assert(offsetof(BinHdr, split) == 4 * NET2_BIN_SPLIT, "split word");
 static_assert(sizeof(BinHdr) == 4 * NET2_BIN_HDR, "header size");
-static_assert(2048 + NET2_BIN_GRID * 8 <= 2 * NET2_SHA2_NBINS, "probe words");
+static_assert(NET2_BIN_CTL + 2048 + NET2_BIN_GRID * 8 <= NET2_BIN_WS_WORDS,
+    "probe words");
+static_assert(NET2_BIN_HDR + 2 * NET2_BIN_SLICES * NET2_SHA2_NBINS <=
+    NET2_BIN_CTL, "histogram slices");
 static_assert(BIN_CTL_STATE < BIN_CTL_PAR && 32 * NET2_BIN_GROUPS <= BIN_CTL_TOP,
     "barrier words");
 enum { BIN_UNDECIDED = 0, BIN_GO = 1, BIN_ABORT = 2 };
@@ -2187,16 +2191,18 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
     const uint32_t *__restrict__ lens, uint64_t n, int blk_shift,
     int lenbytes, uint32_t *__restrict__ ws, uint64_t timeout)
 {
-	__shared__ uint32_t cnt[NET2_BIN_COPIES * NET2_SHA2_NBINS];
+	__shared__ uint32_t cnt[NET2_SHA2_NBINS];
 	__shared__ uint32_t start[NET2_SHA2_NBINS];
 	__shared__ uint32_t wsum[4];
 	__shared__ uint32_t bc[2];
 	BinHdr *h = reinterpret_cast<BinHdr *>(ws);
-	uint32_t *hist0 = ws + NET2_BIN_HDR;			/* [2][NBINS] */
-	uint32_t *ctl0 = hist0 + 2 * NET2_SHA2_NBINS;		/* [2][1024] */
+	uint32_t *hist0 = ws + NET2_BIN_HDR;		/* [2][SLICES][NBINS] */
+	uint32_t *ctl0 = ws + NET2_BIN_CTL;		/* [2][1024] */
 	uint32_t *perm = ws + NET2_BIN_WS_WORDS;
 	const uint32_t G = gridDim.x;
 	const uint64_t ntiles = (n + NET2_BIN_TILE - 1) / NET2_BIN_TILE;
+	constexpr uint32_t HW = NET2_BIN_SLICES * NET2_SHA2_NBINS;
+	const uint32_t slice = blockIdx.x & (NET2_BIN_SLICES - 1);
 
 	/* the first tile's lengths in flight while the header is read */
 	uint32_t len[NET2_BIN_ITEMS];
@@ -2207,9 +2213,8 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		    __HIP_MEMORY_SCOPE_AGENT) == NET2_BIN_MAGIC;
 		bc[1] = ld_agent(&h->epoch);
 	}
-	for (uint32_t b = threadIdx.x; b < NET2_BIN_COPIES * NET2_SHA2_NBINS / 4;
-	    b += blockDim.x)
-		reinterpret_cast<uint4 *>(cnt)[b] = make_uint4(0, 0, 0, 0);
+	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
+		cnt[b] = 0;
 	__syncthreads();
 	if (!bc[0]) {
 		/* not initialised: submission order now, initialise for next */
@@ -2217,9 +2222,11 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		if (blockIdx.x == 0 && threadIdx.x == 0)
 			h->split = (uint32_t)n;
 		if (blockIdx.x == 0) {
-			for (uint32_t w = threadIdx.x; w < 2 * NET2_SHA2_NBINS +
-			    2 * BIN_CTL_PAR; w += blockDim.x)
+			for (uint32_t w = threadIdx.x; w < 2 * HW; w += blockDim.x)
 				hist0[w] = 0;
+			for (uint32_t w = threadIdx.x; w < 2 * BIN_CTL_PAR;
+			    w += blockDim.x)
+				ctl0[w] = 0;
 			if (threadIdx.x == 0)
 				h->epoch = 0;
 			__threadfence();
@@ -2232,23 +2239,22 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 	}
 	BIN_STAMP(0);
 	const uint32_t par = bc[1] & 1;
-	uint32_t *hist = hist0 + par * NET2_SHA2_NBINS;
+	const uint32_t *histp = hist0 + par * HW;	/* all slices */
+	uint32_t *hist = hist0 + par * HW + slice * NET2_SHA2_NBINS;
 	uint32_t *ctl = ctl0 + par * BIN_CTL_PAR;
 	/* the next launch's parity, zeroed: its histogram across the grid, its
 	 * barrier words by workgroup 0 */
-	for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-	    w < NET2_SHA2_NBINS; w += G * blockDim.x)
-		hist0[(par ^ 1) * NET2_SHA2_NBINS + w] = 0;
+	for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < HW;
+	    w += G * blockDim.x)
+		hist0[(par ^ 1) * HW + w] = 0;
 	if (blockIdx.x == 0 && threadIdx.x <= NET2_BIN_GROUPS + 1) {
 		const uint32_t w = threadIdx.x < NET2_BIN_GROUPS ? 32 * threadIdx.x :
 		    threadIdx.x == NET2_BIN_GROUPS ? BIN_CTL_TOP : BIN_CTL_STATE;
 		ctl0[(par ^ 1) * BIN_CTL_PAR + w] = 0;
 	}
 
-	/* 1: this workgroup's histogram (in this lane's copy); the ranks of its
-	 * first tile's packets kept in registers */
-	uint32_t *mine = cnt + (__lane_id() & (NET2_BIN_COPIES - 1)) *
-	    NET2_SHA2_NBINS;
+	/* 1: this workgroup's histogram; the ranks of its first tile's packets
+	 * kept in registers */
 	uint32_t bin0[NET2_BIN_ITEMS], rank0[NET2_BIN_ITEMS];
 	for (uint64_t t = blockIdx.x; t < ntiles; t += G) {
 		const uint64_t i0 = t * NET2_BIN_TILE + threadIdx.x;
@@ -2259,7 +2265,7 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 			const uint32_t bn = bin_of(len[k], blk_shift, lenbytes,
 			    NET2_SHA2_NBINS);
 			const uint32_t r = i0 + (uint64_t)k * 256 < n ?
-			    atomicAdd(&mine[bn], 1u) : 0u;
+			    atomicAdd(&cnt[bn], 1u) : 0u;
 			if (t == blockIdx.x) {
 				bin0[k] = bn;
 				rank0[k] = r;
@@ -2268,20 +2274,11 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 	}
 	__syncthreads();
 	BIN_STAMP(1);
-	/* copies -> their exclusive prefix per bin; the bin's total into the
-	 * global histogram, whose old value is where this workgroup's packets
-	 * start inside the bin */
-	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x) {
-		uint32_t acc = 0;
-#pragma unroll
-		for (int c = 0; c < NET2_BIN_COPIES; c++) {
-			const uint32_t v = cnt[c * NET2_SHA2_NBINS + b];
-			cnt[c * NET2_SHA2_NBINS + b] = acc;
-			acc += v;
-		}
-		start[b] = acc != 0 ? __hip_atomic_fetch_add(&hist[b], acc,
+	/* into the global histogram: the add's old value is where this
+	 * workgroup's packets start inside the bin's slice */
+	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
+		start[b] = cnt[b] != 0 ? __hip_atomic_fetch_add(&hist[b], cnt[b],
 		    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-	}
 	__syncthreads();
 	BIN_STAMP(2);
 
@@ -2328,11 +2325,20 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		 * workgroup's starts, then its packets' places */
 		constexpr int PER = NET2_SHA2_NBINS / 256;
 		const int lane = (int)__lane_id(), wave = (int)(threadIdx.x / 64);
-		uint32_t v[PER], sum = 0;
+		uint32_t v[PER], part[PER], sum = 0;
 #pragma unroll
 		for (int j = 0; j < PER; j++) {
+			uint32_t tot = 0, pp = 0;
+#pragma unroll
+			for (int sl = 0; sl < NET2_BIN_SLICES; sl++) {
+				const uint32_t y = ld_agent(&histp[sl *
+				    NET2_SHA2_NBINS + threadIdx.x * PER + j]);
+				tot += y;
+				pp += (uint32_t)sl < slice ? y : 0u;
+			}
 			v[j] = sum;
-			sum += ld_agent(&hist[threadIdx.x * PER + j]);
+			part[j] = pp;
+			sum += tot;
 		}
 		uint32_t x = sum;
 #pragma unroll
@@ -2350,7 +2356,7 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 #pragma unroll
 		for (int j = 0; j < PER; j++) {
 			const uint32_t b = threadIdx.x * PER + j;
-			start[b] += base + v[j];
+			start[b] += base + v[j] + part[j];
 			/* where the packets of at most two blocks start
 			 * (NET2_SHORT2) */
 			if (blockIdx.x == 0 && b == NET2_SHA2_NBINS - 3)
@@ -2365,8 +2371,7 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 #pragma unroll
 			for (int k = 0; k < NET2_BIN_ITEMS; k++) {
 				const uint64_t i = i0 + (uint64_t)k * 256;
-				const uint32_t pos = start[bin0[k]] +
-				    mine[bin0[k]] + rank0[k];
+				const uint32_t pos = start[bin0[k]] + rank0[k];
 				if (i < n && pos < n)
 					perm[pos] = (uint32_t)i;
 			}
@@ -2408,7 +2413,7 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 __global__ __launch_bounds__(256) void bin_ws_init_kernel(uint32_t *ws)
 {
 	BinHdr *h = reinterpret_cast<BinHdr *>(ws);
-	for (uint32_t w = threadIdx.x; w < 2 * NET2_SHA2_NBINS + 2 * BIN_CTL_PAR;
+	for (uint32_t w = threadIdx.x; w < NET2_BIN_WS_WORDS - NET2_BIN_HDR;
 	    w += blockDim.x)
 		ws[NET2_BIN_HDR + w] = 0;
 	if (threadIdx.x == 0)

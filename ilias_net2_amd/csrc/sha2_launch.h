@@ -25,7 +25,10 @@
  * claim counters in two parities (2 x 2 x NBINS), then perm[n].
  */
 #define NET2_BIN_HDR 16
-#define NET2_BIN_WS_WORDS (NET2_BIN_HDR + 4 * NET2_SHA2_NBINS)
+/* header, two parities of up to eight histogram slices, barrier words and
+ * probe stamps (NET2_BIN_CTL, 4,096 words) */
+#define NET2_BIN_CTL (NET2_BIN_HDR + 16 * NET2_SHA2_NBINS)
+#define NET2_BIN_WS_WORDS (NET2_BIN_CTL + 2 * NET2_SHA2_NBINS)
 /* header word: the binned order's first packet of at most two blocks (the
  * short tail), or n when the order is not binned */
 #define NET2_BIN_SPLIT 6

@@ -175,7 +175,8 @@ def test_side_stream_temporaries(dev, oracle_mod):
     o = torch.from_numpy(offs.astype(np.int64)).to(dev)
     ln = torch.from_numpy(lens.astype(np.int32)).to(dev)
     key = bytes(range(32))
-    ws_bytes = (2 * 2048 + n) * 4
+    from ilias_net2_amd import _lib
+    ws_bytes = _lib.lib().net2_sha2_dev_var_workspace(n)
     side = torch.cuda.Stream(dev)
     torch.cuda.synchronize()
     side.wait_stream(torch.cuda.current_stream(dev))

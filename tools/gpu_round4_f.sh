@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_gpu_binning.py tests/test_gpu_parity.py tests/test_gpu_packet.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/gputest_bin2.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/gputest_bin2.log; [ $rc -ne 0 ] && exit $rc
-for v in probe probec1 probec4; do
+for v in probe probes1; do
   NET2_SHA2_LIB=$PWD/tools/ab/$v.so timeout -k 10 200 python tools/bin_probe.py > gpurun_out/bin_probe_$v.txt 2>&1
   rc=$?; echo "== $v rc=$rc"; grep -v -e Warn -e amdgpu.ids gpurun_out/bin_probe_$v.txt; [ $rc -ne 0 ] && exit $rc
 done
