@@ -246,7 +246,7 @@ struct Sha512HF : Sha512 {
  */
 enum { AMODE_A16 = 0, AMODE_A1 = 1, AMODE_A4 = 2 };
 /*
- * NET2_ONEPATH: the variable-length and HMAC kernels take the A16 block
+ * NET2_ONEPATH256 / NET2_ONEPATH512: the variable-length and HMAC kernels take the A16 block
  * loads (global_load_dwordx4 at the block start) whatever the packet's
  * alignment, relying on the unaligned access mode ROCm sets for gfx9+
  * global memory (tools/unaligned_probe.hip: every byte offset reads the
@@ -254,13 +254,23 @@ enum { AMODE_A16 = 0, AMODE_A1 = 1, AMODE_A4 = 2 };
  * path per kernel instead of three chosen per wave (A16 / A4 / A1).  The
  * tail block keeps its aligned-dword reads (it never touches a byte past
  * the packet).  A misaligned dwordx4 costs the memory pipeline more (a
- * pure load stream at byte offset 1: 59 against 22 us), which these
- * VALU-bound kernels hide: RX verify +1.7 / +2.2 %, burst RX +1.4 /
- * +0.8 %, the rest within +-0.5 % (profiles/round4/ab_*.txt).
+ * pure load stream at byte offset 1: 59 against 22 us).  Per hash family,
+ * from order-flipped A/Bs on separate boxes (profiles/round4/ab_*.txt): the
+ * SHA-512 kernels take the one path (HMAC-SHA512 verify +2.8 %, burst RX
+ * +2 %, c3_512 +0.5 to +1.2 %), the SHA-256 kernels keep the three
+ * (HMAC-SHA256 verify 1.5 % and C3 0.45 % faster with them).
  */
-#ifndef NET2_ONEPATH
-#define NET2_ONEPATH 1
+#ifndef NET2_ONEPATH256
+#define NET2_ONEPATH256 0
 #endif
+#ifndef NET2_ONEPATH512
+#define NET2_ONEPATH512 1
+#endif
+template <class H>
+struct OnePath {
+	static constexpr bool value = sizeof(typename H::word) == 8 ?
+	    NET2_ONEPATH512 != 0 : NET2_ONEPATH256 != 0;
+};
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 /*
@@ -993,7 +1003,8 @@ __device__ __forceinline__ void var_item(uint64_t g,
 	if constexpr (sizeof(typename H::word) == 8)
 		padtab = block_pad512(live, len);
 
-	if (NET2_ONEPATH || __all((reinterpret_cast<uintptr_t>(p) & 15) == 0))
+	if (OnePath<H>::value ||
+	    __all((reinterpret_cast<uintptr_t>(p) & 15) == 0))
 		var_digest<H, AMODE_A16>(p, len, is384, kw, padtab, st);
 	else if (__all((reinterpret_cast<uintptr_t>(p) & 3) == 0))
 		var_digest<H, AMODE_A4>(p, len, is384, kw, padtab, st);
@@ -1012,60 +1023,17 @@ __device__ __forceinline__ void var_item(uint64_t g,
 		store_digest<H::DLEN>(out + i * H::DLEN, o);
 }
 
-/*
- * NET2_SHORT2: in a binned batch, the lanes of the short tail (packets of at
- * most two blocks, counted by the binning: split[0]) take two packets each,
- * so half as many waves run it and each workgroup's fixed start -- for the
- * HMAC kernels the constant table, key block and barriers -- serves twice
- * the packets.  Workgroup-aligned, so every thread of a workgroup loops the
- * same number of times.  Returns the number of packets (0: the whole
- * workgroup exits, its packets are taken by lanes below) and the second
- * position.
- */
-#ifndef NET2_SHORT2
-#define NET2_SHORT2 0
-#endif
-/* SHA-512 kernels only: the second packet costs the SHA-256 kernels a few
- * VGPRs, which at 96 is their fifth wave */
-template <class H>
-struct Short2 {
-	static constexpr bool value = NET2_SHORT2 != 0 &&
-	    sizeof(typename H::word) == 8;
-};
-template <class H>
-__device__ __forceinline__ int short2_reps(const uint32_t *split,
-    const uint32_t *perm, uint64_t n, uint64_t g, uint64_t &g2)
-{
-	if (!Short2<H>::value || perm == nullptr || split == nullptr)
-		return 1;
-	const uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x;
-	const uint64_t s0 = ((uint64_t)split[0] + 255) / 256 * 256;
-	if (s0 >= n || b0 < s0)
-		return 1;
-	const uint64_t half = ((n - s0 + 1) / 2 + 255) / 256 * 256;
-	if (b0 >= s0 + half)
-		return 0;
-	g2 = g + half;
-	return 2;
-}
-
 template <class H>
 __global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(VarWaves<H>::value))) void var_kernel(const uint8_t *__restrict__ base,
     const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
     const uint32_t *__restrict__ perm, uint64_t n, uint8_t *__restrict__ out,
-    uint32_t dlen, int is384, const uint32_t *__restrict__ split)
+    uint32_t dlen, int is384)
 {
-	const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	uint64_t g2 = 0;
-	const int reps = short2_reps<H>(split, perm, n, g, g2);
-	if (reps == 0)
-		return;
 	if (sizeof(typename H::word) == 8)
 		k512_lds_fill();
-	var_item<H>(g, base, offsets, lens, perm, n, out, dlen, is384);
-	if (Short2<H>::value && reps == 2)
-		var_item<H>(g2, base, offsets, lens, perm, n, out, dlen, is384);
+	var_item<H>((uint64_t)blockIdx.x * blockDim.x + threadIdx.x, base,
+	    offsets, lens, perm, n, out, dlen, is384);
 }
 
 /* ---- HMAC (RFC 2104) ------------------------------------------------------ */
@@ -1314,7 +1282,7 @@ __device__ __forceinline__ void hmac_item(uint64_t g,
 	}
 	typename H::State st;
 	const uintptr_t pa = reinterpret_cast<uintptr_t>(p);
-	const int amode = NET2_ONEPATH || __all((pa & 15) == 0) ? AMODE_A16 :
+	const int amode = OnePath<H>::value || __all((pa & 15) == 0) ? AMODE_A16 :
 	    __all((pa & 3) == 0) ? AMODE_A4 : AMODE_A1;
 	/* a variable-layout wave (SHA-256) or workgroup (SHA-512) of one
 	 * whole-block inner length (key block included) takes its inner pad
@@ -1394,18 +1362,13 @@ __attribute__((amdgpu_waves_per_eu(HmacWaves<H, MODE>::value))) void hmac_kernel
     const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
     const uint32_t *__restrict__ perm, uint64_t stride, uint32_t fixed_len,
     uint64_t n, uint8_t *__restrict__ out, uint32_t dlen, int is384,
-    HKey<H::NW32> key, PadKW<typename H::word> pad, BurstArgs rx,
-    const uint32_t *__restrict__ split)
+    HKey<H::NW32> key, PadKW<typename H::word> pad, BurstArgs rx)
 {
 	constexpr int NW32 = H::NW32;
 	/* [0..1]: the key's ipad / opad midstates; [2..3]: the alternate rx
 	 * key's (HMAC_BURST_RX with rx.alt) */
 	__shared__ uint32_t mid[4][16];
 	const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	uint64_t g2 = 0;
-	const int reps = short2_reps<H>(split, perm, n, g, g2);
-	if (reps == 0)
-		return;		/* the whole workgroup: lanes below take its packets */
 	if (sizeof(typename H::word) == 8) {
 		if (PADCONST)
 			k512_lds_fill_pad(pad);
@@ -1436,9 +1399,6 @@ __attribute__((amdgpu_waves_per_eu(HmacWaves<H, MODE>::value))) void hmac_kernel
 	__syncthreads();
 	hmac_item<H, PADCONST, MODE>(g, base, offsets, lens, perm, stride,
 	    fixed_len, n, out, dlen, is384, pad, rx, mid);
-	if (Short2<H>::value && reps == 2)
-		hmac_item<H, PADCONST, MODE>(g2, base, offsets, lens, perm, stride,
-		    fixed_len, n, out, dlen, is384, pad, rx, mid);
 }
 
 /* ---- coalesced small jobs (sha2_coalesce.cpp) ------------------------------- */
@@ -2155,11 +2115,9 @@ static_assert(NET2_BIN_SLICES >= 1 && NET2_BIN_SLICES <= 8 &&
 
 struct BinHdr {
 	uint64_t magic;
-	uint32_t epoch, rsv[3];
-	uint32_t split;		/* word NET2_BIN_SPLIT */
-	uint32_t pad[NET2_BIN_HDR - 7];
+	uint32_t epoch;
+	uint32_t pad[NET2_BIN_HDR - 3];
 };
-static_assert(offsetof(BinHdr, split) == 4 * NET2_BIN_SPLIT, "split word");
 static_assert(sizeof(BinHdr) == 4 * NET2_BIN_HDR, "header size");
 static_assert(NET2_BIN_CTL + 2048 + NET2_BIN_GRID * 8 <= NET2_BIN_WS_WORDS,
     "probe words");
@@ -2219,8 +2177,6 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 	if (!bc[0]) {
 		/* not initialised: submission order now, initialise for next */
 		bin_identity(perm, n, ntiles);
-		if (blockIdx.x == 0 && threadIdx.x == 0)
-			h->split = (uint32_t)n;
 		if (blockIdx.x == 0) {
 			for (uint32_t w = threadIdx.x; w < 2 * HW; w += blockDim.x)
 				hist0[w] = 0;
@@ -2354,14 +2310,8 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		for (int w = 0; w < wave; w++)
 			base += wsum[w];
 #pragma unroll
-		for (int j = 0; j < PER; j++) {
-			const uint32_t b = threadIdx.x * PER + j;
-			start[b] += base + v[j] + part[j];
-			/* where the packets of at most two blocks start
-			 * (NET2_SHORT2) */
-			if (blockIdx.x == 0 && b == NET2_SHA2_NBINS - 3)
-				h->split = base + v[j];
-		}
+		for (int j = 0; j < PER; j++)
+			start[threadIdx.x * PER + j] += base + v[j] + part[j];
 		__syncthreads();
 		BIN_STAMP(5);
 		if (ntiles <= G) {
@@ -2404,7 +2354,6 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		if (threadIdx.x == 0) {	/* re-initialise at the next launch */
 			__hip_atomic_store(&h->magic, 0ull, __ATOMIC_RELAXED,
 			    __HIP_MEMORY_SCOPE_AGENT);
-			h->split = (uint32_t)n;
 		}
 	}
 }
@@ -2664,21 +2613,19 @@ hipError_t net2_launch_var(int alg, const uint8_t *base,
 	const int is384 = alg == NET2_ALG_SHA384;
 	const uint32_t dlen = s256 ? 32 : is384 ? 48 : 64;
 	uint32_t *perm = nullptr;
-	const uint32_t *split = nullptr;
 
 	if (ws != nullptr) {
 		hipError_t e = net2_bin_order(alg, lens, n, ws, s);
 		if (e != hipSuccess)
 			return e;
 		perm = ws + NET2_BIN_WS_WORDS;
-		split = ws + NET2_BIN_SPLIT;
 	}
 	if (s256)
 		var_kernel<Sha256V><<<grid_for(n), 256, 0, s>>>(base, offsets,
-		    lens, perm, n, out, dlen, 0, split);
+		    lens, perm, n, out, dlen, 0);
 	else
 		var_kernel<Sha512V><<<grid_for(n), 256, 0, s>>>(base, offsets,
-		    lens, perm, n, out, dlen, is384, split);
+		    lens, perm, n, out, dlen, is384);
 	return hipGetLastError();
 }
 /* H without the pair loop: the VERIFY kernel measured 1.5 % faster without
@@ -2693,26 +2640,25 @@ template <class H>
 static void launch_hmac_var_mode(int mode, unsigned grid, hipStream_t s,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
     const uint32_t *perm, uint64_t n, uint8_t *out, uint32_t dlen, int is384,
-    HKey<H::NW32> k, PadKW<typename H::word> pad, BurstArgs rx,
-    const uint32_t *split)
+    HKey<H::NW32> k, PadKW<typename H::word> pad, BurstArgs rx)
 {
 	if (mode == HMAC_SIGN)
 		hmac_kernel<H, false, HMAC_SIGN><<<grid, 256, 0, s>>>(base, offsets,
-		    lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx, split);
+		    lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx);
 	else if (mode == HMAC_VERIFY)
 		hmac_kernel<typename NoPair<H>::type, false, HMAC_VERIFY>
 		    <<<grid, 256, 0, s>>>(base, offsets, lens, perm, 0, 0, n, out,
-		    dlen, is384, k, pad, rx, split);
+		    dlen, is384, k, pad, rx);
 	else if (mode == HMAC_BURST_RX)
 		hmac_kernel<typename NoPair<H>::type, false, HMAC_BURST_RX>
 		    <<<grid, 256, 0, s>>>(base, offsets, lens, perm, 0, 0, n, out,
-		    dlen, is384, k, pad, rx, split);
+		    dlen, is384, k, pad, rx);
 	else if (mode == HMAC_BURST_TX)
 		hmac_kernel<H, false, HMAC_BURST_TX><<<grid, 256, 0, s>>>(base,
-		    offsets, lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx, split);
+		    offsets, lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx);
 	else
 		hmac_kernel<H, false><<<grid, 256, 0, s>>>(base, offsets,
-		    lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx, split);
+		    lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx);
 }
 
 hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
@@ -2739,13 +2685,11 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 	for (size_t i = 0; i < keylen; i++)
 		kb[i] = key[i];
 	uint32_t *perm = nullptr;
-	const uint32_t *split = nullptr;
 	if (offsets != nullptr && ws != nullptr) {
 		hipError_t e = net2_bin_order(halg, lens, n, ws, s);
 		if (e != hipSuccess)
 			return e;
 		perm = ws + NET2_BIN_WS_WORDS;
-		split = ws + NET2_BIN_SPLIT;
 	}
 	const unsigned grid = grid_for(n);
 	const bool padconst = offsets == nullptr && fixed_len % blk == 0;
@@ -2759,13 +2703,13 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 		if (padconst) {
 			pad_kw256(ibits, pad);
 			hmac_kernel<Sha256H, true><<<grid, 256, 0, s>>>(base, offsets,
-			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad, rx, split);
+			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad, rx);
 		} else if (offsets != nullptr) {
 			launch_hmac_var_mode<Sha256H>(mode, grid, s, base, offsets,
-			    lens, perm, n, out, dlen, 0, k, pad, rx, split);
+			    lens, perm, n, out, dlen, 0, k, pad, rx);
 		} else {
 			hmac_kernel<Sha256H, false><<<grid, 256, 0, s>>>(base, offsets,
-			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad, rx, split);
+			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad, rx);
 		}
 	} else {
 		HKey<32> k;
@@ -2776,13 +2720,13 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 		if (padconst) {
 			pad_kw512(ibits, pad);
 			hmac_kernel<Sha512HF, true><<<grid, 256, 0, s>>>(base, offsets,
-			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad, rx, split);
+			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad, rx);
 		} else if (offsets != nullptr) {
 			launch_hmac_var_mode<Sha512H>(mode, grid, s, base, offsets,
-			    lens, perm, n, out, dlen, is384, k, pad, rx, split);
+			    lens, perm, n, out, dlen, is384, k, pad, rx);
 		} else {
 			hmac_kernel<Sha512HF, false><<<grid, 256, 0, s>>>(base, offsets,
-			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad, rx, split);
+			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad, rx);
 		}
 	}
 	return hipGetLastError();

@@ -29,10 +29,6 @@
  * probe stamps (NET2_BIN_CTL, 4,096 words) */
 #define NET2_BIN_CTL (NET2_BIN_HDR + 16 * NET2_SHA2_NBINS)
 #define NET2_BIN_WS_WORDS (NET2_BIN_CTL + 2 * NET2_SHA2_NBINS)
-/* header word: the binned order's first packet of at most two blocks (the
- * short tail), or n when the order is not binned */
-#define NET2_BIN_SPLIT 6
-
 /* Fixed-stride batch; base/out in device memory, async on s. */
 hipError_t net2_launch_fixed(int alg, const uint8_t *base, uint64_t stride,
     uint32_t len, uint64_t n, uint8_t *out, hipStream_t s);

@@ -3,7 +3,7 @@
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_binning.py tests/test_gpu_parity.py tests/test_gpu_packet.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/gputest_bin2.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_binning.py tests/test_gpu_parity.py tests/test_gpu_packet.py tests/test_gpu_dgram.py tests/test_gpu_multidev.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/gputest_bin2.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/gputest_bin2.log; [ $rc -ne 0 ] && exit $rc
 for v in probe probes1; do
   NET2_SHA2_LIB=$PWD/tools/ab/$v.so timeout -k 10 200 python tools/bin_probe.py > gpurun_out/bin_probe_$v.txt 2>&1
@@ -19,5 +19,5 @@ for v in default bin3; do
 done
 unset NET2_SHA2_LIB
 rm -f tools/ab/probe*.so
-CFGS=${CFGS:-"c3 c3_512 hmac512_verify_mtu burst_rx"} REPS=${REPS:-"1 2"} bash tools/gpu_ab_lib.sh > /dev/null
+CFGS=${CFGS:-"c3 c3_512 hmac_mtu hmac_verify_mtu hmac512_verify_mtu burst_rx"} REPS=${REPS:-"1 2"} bash tools/gpu_ab_lib.sh > /dev/null
 cat gpurun_out/ab_lib.txt
