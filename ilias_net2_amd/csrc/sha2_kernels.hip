@@ -2031,9 +2031,8 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(
  * workgroups (each loops over its 4,096-packet tiles):
  *   1. LDS histogram of its tiles, each packet's rank in its bin kept in
  *      registers (the LDS atomic's return value), then one device-scope
- *      fetch-add per touched bin into the global histogram (its slice of
- *      it), whose old value is where the workgroup's packets start inside
- *      that bin, after the slices before its own;
+ *      fetch-add per touched bin into the global histogram, whose old value
+ *      is where the workgroup's packets start inside that bin;
  *   2. a grid barrier in two levels: 16 group counters (workgroup
  *      blockIdx & 15, one XCD each), the last of each group arrives at a top
  *      counter, the last of those flips `state` to GO and bumps the epoch;
@@ -2081,21 +2080,10 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(
 #ifndef NET2_BIN_SPIN_SLEEP
 #define NET2_BIN_SPIN_SLEEP 2
 #endif
-/*
- * Global histogram slices (power of two, <= 8): workgroup w adds into slice
- * w & (S-1) (its XCD), so each bin's device-scope adds queue on S addresses
- * instead of one; a workgroup's start inside a bin is then the slices
- * before its own plus its add's old value in its slice.
- */
-#ifndef NET2_BIN_SLICES
-#define NET2_BIN_SLICES 8
-#endif
-static_assert(NET2_BIN_SLICES >= 1 && NET2_BIN_SLICES <= 8 &&
-    (NET2_BIN_SLICES & (NET2_BIN_SLICES - 1)) == 0, "slices");
 #define NET2_BIN_GROUPS 16
 /*
- * Barrier words, per parity, in the workspace after the histograms (two
- * parities of up to eight slices; each word on its own 128-byte line): group counters at 32 g, the top counter
+ * Barrier words, per parity, in the workspace after the two histograms
+ * (each word on its own 128-byte line): group counters at 32 g, the top counter
  * at 512, the state at 544.  Words 2,048-4,095 of the area hold the probe
  * stamps (NET2_BIN_PROBE=1, tools/bin_probe.py: thread 0 of every
  * workgroup stamps the 100 MHz clock at eight points).
@@ -2121,8 +2109,8 @@ struct BinHdr {
 static_assert(sizeof(BinHdr) == 4 * NET2_BIN_HDR, "header size");
 static_assert(NET2_BIN_CTL + 2048 + NET2_BIN_GRID * 8 <= NET2_BIN_WS_WORDS,
     "probe words");
-static_assert(NET2_BIN_HDR + 2 * NET2_BIN_SLICES * NET2_SHA2_NBINS <=
-    NET2_BIN_CTL, "histogram slices");
+static_assert(NET2_BIN_HDR + 2 * NET2_SHA2_NBINS <= NET2_BIN_CTL,
+    "histograms");
 static_assert(BIN_CTL_STATE < BIN_CTL_PAR && 32 * NET2_BIN_GROUPS <= BIN_CTL_TOP,
     "barrier words");
 enum { BIN_UNDECIDED = 0, BIN_GO = 1, BIN_ABORT = 2 };
@@ -2154,13 +2142,12 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 	__shared__ uint32_t wsum[4];
 	__shared__ uint32_t bc[2];
 	BinHdr *h = reinterpret_cast<BinHdr *>(ws);
-	uint32_t *hist0 = ws + NET2_BIN_HDR;		/* [2][SLICES][NBINS] */
+	uint32_t *hist0 = ws + NET2_BIN_HDR;		/* [2][NBINS] */
 	uint32_t *ctl0 = ws + NET2_BIN_CTL;		/* [2][1024] */
 	uint32_t *perm = ws + NET2_BIN_WS_WORDS;
 	const uint32_t G = gridDim.x;
 	const uint64_t ntiles = (n + NET2_BIN_TILE - 1) / NET2_BIN_TILE;
-	constexpr uint32_t HW = NET2_BIN_SLICES * NET2_SHA2_NBINS;
-	const uint32_t slice = blockIdx.x & (NET2_BIN_SLICES - 1);
+	constexpr uint32_t HW = NET2_SHA2_NBINS;
 
 	/* the first tile's lengths in flight while the header is read */
 	uint32_t len[NET2_BIN_ITEMS];
@@ -2195,8 +2182,7 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 	}
 	BIN_STAMP(0);
 	const uint32_t par = bc[1] & 1;
-	const uint32_t *histp = hist0 + par * HW;	/* all slices */
-	uint32_t *hist = hist0 + par * HW + slice * NET2_SHA2_NBINS;
+	uint32_t *hist = hist0 + par * HW;
 	uint32_t *ctl = ctl0 + par * BIN_CTL_PAR;
 	/* the next launch's parity, zeroed: its histogram across the grid, its
 	 * barrier words by workgroup 0 */
@@ -2231,7 +2217,7 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 	__syncthreads();
 	BIN_STAMP(1);
 	/* into the global histogram: the add's old value is where this
-	 * workgroup's packets start inside the bin's slice */
+	 * workgroup's packets start inside the bin */
 	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
 		start[b] = cnt[b] != 0 ? __hip_atomic_fetch_add(&hist[b], cnt[b],
 		    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
@@ -2281,20 +2267,11 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		 * workgroup's starts, then its packets' places */
 		constexpr int PER = NET2_SHA2_NBINS / 256;
 		const int lane = (int)__lane_id(), wave = (int)(threadIdx.x / 64);
-		uint32_t v[PER], part[PER], sum = 0;
+		uint32_t v[PER], sum = 0;
 #pragma unroll
 		for (int j = 0; j < PER; j++) {
-			uint32_t tot = 0, pp = 0;
-#pragma unroll
-			for (int sl = 0; sl < NET2_BIN_SLICES; sl++) {
-				const uint32_t y = ld_agent(&histp[sl *
-				    NET2_SHA2_NBINS + threadIdx.x * PER + j]);
-				tot += y;
-				pp += (uint32_t)sl < slice ? y : 0u;
-			}
 			v[j] = sum;
-			part[j] = pp;
-			sum += tot;
+			sum += ld_agent(&hist[threadIdx.x * PER + j]);
 		}
 		uint32_t x = sum;
 #pragma unroll
@@ -2311,7 +2288,7 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 			base += wsum[w];
 #pragma unroll
 		for (int j = 0; j < PER; j++)
-			start[threadIdx.x * PER + j] += base + v[j] + part[j];
+			start[threadIdx.x * PER + j] += base + v[j];
 		__syncthreads();
 		BIN_STAMP(5);
 		if (ntiles <= G) {

@@ -25,9 +25,9 @@
  * claim counters in two parities (2 x 2 x NBINS), then perm[n].
  */
 #define NET2_BIN_HDR 16
-/* header, two parities of up to eight histogram slices, barrier words and
- * probe stamps (NET2_BIN_CTL, 4,096 words) */
-#define NET2_BIN_CTL (NET2_BIN_HDR + 16 * NET2_SHA2_NBINS)
+/* header, the histogram's two parities, barrier words and probe stamps
+ * (NET2_BIN_CTL, 4,096 words) */
+#define NET2_BIN_CTL (NET2_BIN_HDR + 2 * NET2_SHA2_NBINS)
 #define NET2_BIN_WS_WORDS (NET2_BIN_CTL + 2 * NET2_SHA2_NBINS)
 /* Fixed-stride batch; base/out in device memory, async on s. */
 hipError_t net2_launch_fixed(int alg, const uint8_t *base, uint64_t stride,

@@ -69,13 +69,13 @@ def test_workspace_lifecycle(dev, oracle_mod, alg):
         else:
             assert (np.diff(bl[order]) <= 0).all(), call
     # epoch counts the binned launches (header word 2); the barrier words
-    # (after the header and two parities of eight 2,048-bin histogram
-    # slices, 1,024 per parity: group counters every 32 words, top counter
+    # (after the header and the two parities of the 2,048-bin histogram,
+    # 1,024 per parity: group counters every 32 words, top counter
     # at 512, state at 544) -- the last launch's parity (0) decided GO with
     # every workgroup arrived, the next one's zeroed
     w = ws.cpu().numpy().view(np.uint32)
     assert w[2] == 5, w[:8]
-    ctl0 = 16 + 16 * 2048
+    ctl0 = 16 + 2 * 2048
     ctl = w[ctl0:ctl0 + 2 * 1024].reshape(2, 1024)
     G = min(256, (n + 4095) // 4096)
     assert ctl[0, 544] == 1 and ctl[0, 512] == min(G, 16), ctl[0, [512, 544]]

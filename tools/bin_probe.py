@@ -41,7 +41,7 @@ def main():
         for _ in range(20):
             batch.digest_var(alg, d, o, ln, workspace=ws)
         torch.cuda.synchronize()
-        base = 16 + 16 * nb + 2048         # after the histograms, barrier words
+        base = 16 + 2 * nb + 2048          # after the histograms, barrier words
         st = ws.cpu().numpy().view(np.uint32)[base:base + 256 * 8]
         st = st.reshape(256, 8).astype(np.int64)
         st = (st - st[:, 0].min()) & 0xffffffff
