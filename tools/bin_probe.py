@@ -54,7 +54,7 @@ def main():
                   f"  max {c.max():7.2f}")
         last = int(np.argmax(st[:, 3]))
         print(f"  last arriver: workgroup {last}, its stamps "
-              f"{[round(v / 100, 2) for v in st[last]]}")
+              f"{[round(float(v) / 100, 2) for v in st[last, :7]]}")
         assert hdr >= 16
 
 
