@@ -478,6 +478,7 @@ def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
             j += 1
         else:
             step()
+    enqueue_ms = (time.perf_counter() - t0) * 1e3
     # shader clock while the queued steps run, sampled every ~2 ms by a
     # helper thread (a sysfs read can take a millisecond: kept off the
     # thread whose synchronize ends the timed region)
@@ -521,6 +522,7 @@ def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
     res = {"n": n, "dlen": dlen, "payload": inp["payload"], "elapsed": elapsed,
            "ms_per_step": elapsed * 1e3 / steps, "launch_ms": launch_ms,
            "ms_per_step_local": local_ms,
+           "host_enqueue_ms": enqueue_ms,
            "event_pairs": len(ev),
            "per_launch_bytes": per_launch,
            "sclk_during_mhz": (round(sum(samples) / len(samples)) if samples else None),
@@ -751,6 +753,9 @@ def main():
         line["roofline_valu"] = valu
     gpu["sclk_mhz_during_timed_steps"] = r["sclk_during_mhz"]
     line["gpu"] = gpu
+    # host time to queue the timed steps (rank 0's): near the whole timed
+    # region means the launches, not the GPU, set the pace
+    line["host_enqueue_ms"] = round(r["host_enqueue_ms"], 3)
     ranks = gather_ranks(rank_record(rank, gpu, r["ms_per_step_local"]), ws)
     if ws > 1:
         sf = scale_fields(ranks, args.dist_backend)
