@@ -102,6 +102,38 @@ def test_prepared_workspace_bins_from_the_first_call(dev, oracle_mod):
     assert L.net2_sha2_workspace_init(None, 0, None) == 22
 
 
+@pytest.mark.parametrize("n", [1, 4096, 4097, 15 * 4096 + 7, 16 * 4096,
+                               17 * 4096 + 1, 33 * 4096 + 5])
+def test_grid_sizes_around_the_barrier_groups(dev, oracle_mod, n):
+    """G = 1 .. 34 workgroups: groups of one, groups of two, a partial
+    top level (G < 16) -- each launch decides GO with every workgroup
+    counted once, two launches in a row (both parities)."""
+    from ilias_net2_amd import _lib, batch
+    L = _lib.lib()
+    lens = synth.mixed_lengths(650 + n % 97, n, choices=(0, 64, 300, 1500))
+    data, offs = synth.packed(651, lens)
+    if data.size == 0:
+        data = np.zeros(1, dtype=np.uint8)
+    want = oracle_mod.batch(3, data, offsets=offs, lens=lens, nthreads=16)
+    d = torch.from_numpy(data).to(dev)
+    o = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    ln = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    ws = batch.var_workspace(n, dev)
+    G = min(256, (n + 4095) // 4096)
+    for call in range(2):
+        got = batch.digest_var(3, d, o, ln, workspace=ws)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy(), want), (n, call)
+        order = _order(ws, L, n)
+        assert np.array_equal(np.sort(order), np.arange(n))
+        assert (np.diff(_blocks(lens, 3)[order]) <= 0).all()
+        w = ws.cpu().numpy().view(np.uint32)
+        assert w[2] == call + 1
+        ctl = w[16 + 2 * 2048:16 + 2 * 2048 + 2 * 1024].reshape(2, 1024)[call & 1]
+        assert ctl[544] == 1 and ctl[512] == min(G, 16), (n, call, ctl[[512, 544]])
+        assert ctl[0:512:32].sum() == G
+
+
 def test_many_tiles_per_workgroup(dev, oracle_mod):
     """3 M packets: 733 tiles over the 256-workgroup persistent grid (each
     workgroup bins three tiles), lengths over seven bins."""
