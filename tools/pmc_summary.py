@@ -36,14 +36,23 @@ KERNEL = {"c2": "fixed_kernel<net2::dev::Sha256", "c4": "fixed_kernel<net2::dev:
           "hmac_verify_mtu": "hmac_kernel<net2::dev::Sha256",
           "hmac512_verify_mtu": "hmac_kernel<net2::dev::Sha512",
           "burst_rx": "hmac_kernel<net2::dev::Sha512", "burst_tx": "hmac_kernel<net2::dev::Sha512"}
+# the timed kernel's HMAC mode (the template's last argument), where the
+# config also runs another mode once, untimed: the signing pass before a
+# verify config, the encode before burst RX
+MODE = {"hmac_verify_mtu": ", 2>", "hmac512_verify_mtu": ", 2>", "burst_rx": ", 3>",
+        "burst_tx": ", 4>"}
 
 
-def per_dispatch(path, pattern):
+def matches(name, cfg):
+    return KERNEL[cfg] in name and MODE.get(cfg, "") in name
+
+
+def per_dispatch(path, cfg):
     """{counter: [per-dispatch totals]} and [durations ns] for one kernel."""
     vals, durs = {}, {}
     with open(path) as f:
         for r in csv.DictReader(f):
-            if pattern not in r["Kernel_Name"]:
+            if not matches(r["Kernel_Name"], cfg):
                 continue
             d = r["Dispatch_Id"]
             key = (d, r["Counter_Name"])
@@ -70,19 +79,19 @@ def main():
         path = os.path.join(args.src, f"pmc_{args.cfg}_{tag}", "run_counter_collection.csv")
         if not os.path.exists(path):
             continue
-        c, d = per_dispatch(path, pat)
+        c, d = per_dispatch(path, args.cfg)
         for k, v in c.items():
             counters[k] = v
         durs_all += d
     med = {k: statistics.median(v) for k, v in counters.items()}
-    res = {"config": args.cfg, "kernel": pat, "dispatches_per_pass": len(durs_all) and
+    res = {"config": args.cfg, "kernel": pat + MODE.get(args.cfg, ""), "dispatches_per_pass": len(durs_all) and
            max(len(v) for v in counters.values()),
            "counters_median_per_launch": med}
     stats_csv = os.path.join(args.src, f"prof_{args.cfg}", "run_kernel_stats.csv")
     if os.path.exists(stats_csv):
         with open(stats_csv) as f:
             for r in csv.DictReader(f):
-                if pat in r["Name"]:
+                if matches(r["Name"], args.cfg):
                     res["trace_avg_ns"] = float(r["AverageNs"])
                     res["trace_calls"] = int(r["Calls"])
         dst = os.path.join(ROOT, "profiles", args.round)
