@@ -18,7 +18,7 @@ import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 for r in rows:
     nm = r["Name"]
-    if any(k in nm for k in ("hmac_kernel", "burst_final", "bin_count", "bin_scatter", "fillBuffer")):
+    if any(k in nm for k in ("hmac_kernel", "burst_final", "bin_count", "bin_scatter", "bin_onepass", "fillBuffer")):
         print(f"  {sys.argv[2]:14s} {nm.split('(')[0][-60:]:60s} calls {r['Calls']:>5s} avg_us {float(r['AverageNs'])/1e3:8.2f}")
 EOF
 done
