@@ -1825,68 +1825,18 @@ __device__ __forceinline__ uint32_t bin_of(uint32_t len, int blk_shift,
 	return nbins - 1 - b;	/* descending block count */
 }
 
-/* Packets per thread in the binning kernels: one workgroup bins a tile of
- * 256 x 16 = 4,096 packets (256 workgroups per 1 M packets).  Every
- * workgroup pays a fixed cost (clearing and flushing the 2,048-bin LDS
- * histogram, the scatter's histogram scan, its global atomics), so fewer,
- * larger tiles win down to 4,096 packets; 2,048 and 8,192 measured slower
- * (profiles/round1/binning_time_ab.txt). */
+/* Packets per thread in the binning: one workgroup bins a tile of
+ * 256 x 16 = 4,096 packets (the whole 256-workgroup grid covers 1 M packets
+ * with one tile each).  Every workgroup pays a fixed cost (clearing the
+ * 2,048-bin LDS histogram, the histogram scan, its global atomics), so
+ * fewer, larger tiles win down to 4,096 packets; 2,048 and 8,192 measured
+ * slower (profiles/round1/binning_time_ab.txt, on the three-launch binning
+ * of rounds 1-3). */
 #ifndef NET2_BIN_ITEMS
 #define NET2_BIN_ITEMS 16
 #endif
 #define NET2_BIN_TILE (256 * NET2_BIN_ITEMS)
-/*
- * 1: no separate scan launch -- every scatter workgroup scans the 2,048-bin
- * histogram itself (8 KiB, L2-resident) and claims its ranges from a zeroed
- * per-bin counter; 0: count, scan (one workgroup), scatter.
- */
-#ifndef NET2_BIN_FUSED
-#define NET2_BIN_FUSED 1
-#endif
-
-/*
- * Wave-aggregated LDS counter add: the lanes of a wave that carry the same
- * key elect one leader that adds the group's size once (a {64,512,1500}
- * batch puts 3 keys in a wave: 3 LDS atomics instead of 64).  Returns the
- * counter's value before the group's add plus this lane's rank in its group.
- */
-/* 0: one LDS atomic per lane (shipped: binning 25 -> 16 us per 1 M packets
- * with 4,096-packet tiles, profiles/round1/binning_time_ab.txt); 1: the
- * wave-aggregated loop below (ballot per distinct key, one atomic each). */
-#ifndef NET2_BIN_WAVEAGG
-#define NET2_BIN_WAVEAGG 0
-#endif
-__device__ __forceinline__ uint32_t wave_rank_add(uint32_t *ctr, uint32_t key,
-    bool active)
-{
-	if (!NET2_BIN_WAVEAGG) {
-		/* one LDS atomic per lane; the LDS serialises equal addresses */
-		return active ? atomicAdd(&ctr[key], 1u) : 0u;
-	}
-	uint64_t todo = __ballot(active);
-	const uint64_t below = __lanemask_lt();
-	const int lane = (int)__lane_id();
-	uint32_t rank = 0;
-	while (todo != 0) {
-		const int leader = __ffsll((unsigned long long)todo) - 1;
-		const uint32_t k = __shfl(key, leader);
-		const uint64_t grp = __ballot(active && key == k);
-		uint32_t base = 0;
-		if (lane == leader)
-			base = atomicAdd(&ctr[k], (uint32_t)__popcll(grp));
-		base = __shfl(base, leader);
-		if (active && key == k)
-			rank = base + (uint32_t)__popcll(grp & below);
-		todo &= ~grp;
-	}
-	return rank;
-}
-
-/*
- * A thread's NET2_BIN_ITEMS lengths, all loads issued before any is used:
- * behind the data-dependent loop of wave_rank_add the compiler would
- * otherwise wait out one memory latency per item.
- */
+/* A thread's NET2_BIN_ITEMS lengths, all loads issued before any is used. */
 __device__ __forceinline__ void load_lens(const uint32_t *__restrict__ lens,
     uint64_t n, uint64_t i0, uint32_t (&len)[NET2_BIN_ITEMS])
 {
@@ -1897,137 +1847,9 @@ __device__ __forceinline__ void load_lens(const uint32_t *__restrict__ lens,
 	}
 }
 
-__global__ __launch_bounds__(256) void bin_count_kernel(
-    const uint32_t *__restrict__ lens, uint64_t n, int blk_shift,
-    int lenbytes, uint32_t *__restrict__ hist)
-{
-	__shared__ uint32_t lh[NET2_SHA2_NBINS];
-	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
-		lh[b] = 0;
-	__syncthreads();
-	const uint64_t i0 = (uint64_t)blockIdx.x * NET2_BIN_TILE + threadIdx.x;
-	uint32_t len[NET2_BIN_ITEMS];
-	load_lens(lens, n, i0, len);
-#pragma unroll
-	for (int k = 0; k < NET2_BIN_ITEMS; k++) {
-		const bool live = i0 + (uint64_t)k * 256 < n;
-		const uint32_t bin = live ? bin_of(len[k], blk_shift, lenbytes,
-		    NET2_SHA2_NBINS) : 0;
-		(void)wave_rank_add(lh, bin, live);
-	}
-	__syncthreads();
-	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
-		if (lh[b] != 0)
-			atomicAdd(&hist[b], lh[b]);
-}
-
-/* Exclusive scan of the histogram into bin cursors; one 1024-thread block. */
-__global__ __launch_bounds__(1024) void bin_scan_kernel(
-    const uint32_t *__restrict__ hist, uint32_t *__restrict__ cursor)
-{
-	__shared__ uint32_t part[1024];
-	constexpr int PER = NET2_SHA2_NBINS / 1024;
-	uint32_t loc[PER], s = 0;
-#pragma unroll
-	for (int j = 0; j < PER; j++) {
-		loc[j] = s;
-		s += hist[threadIdx.x * PER + j];
-	}
-	part[threadIdx.x] = s;
-	__syncthreads();
-	for (int off = 1; off < 1024; off <<= 1) {
-		uint32_t v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0;
-		__syncthreads();
-		part[threadIdx.x] += v;
-		__syncthreads();
-	}
-	uint32_t base = threadIdx.x ? part[threadIdx.x - 1] : 0;
-#pragma unroll
-	for (int j = 0; j < PER; j++)
-		cursor[threadIdx.x * PER + j] = base + loc[j];
-}
-
 /*
- * Exclusive prefix of the global histogram into LDS (NET2_BIN_FUSED): each
- * of the 256 threads sums 8 consecutive bins, a shuffle scan per wave and
- * the four wave totals give its offset.
- */
-__device__ __forceinline__ void hist_prefix_lds(const uint32_t *__restrict__ hist,
-    uint32_t *pre)
-{
-	__shared__ uint32_t wsum[4];
-	constexpr int PER = NET2_SHA2_NBINS / 256;
-	const int lane = (int)__lane_id(), wave = (int)(threadIdx.x / 64);
-	uint32_t v[PER], s = 0;
-#pragma unroll
-	for (int j = 0; j < PER; j++) {
-		const uint32_t t = hist[threadIdx.x * PER + j];
-		v[j] = s;
-		s += t;
-	}
-	uint32_t x = s;
-#pragma unroll
-	for (int off = 1; off < 64; off <<= 1) {
-		const uint32_t y = __shfl_up(x, off);
-		if (lane >= off)
-			x += y;
-	}
-	if (lane == 63)
-		wsum[wave] = x;
-	__syncthreads();
-	uint32_t base = x - s;
-	for (int w = 0; w < wave; w++)
-		base += wsum[w];
-#pragma unroll
-	for (int j = 0; j < PER; j++)
-		pre[threadIdx.x * PER + j] = base + v[j];
-}
-
-/*
- * Scatter packet indices to their bin.  Each block ranks its own packets
- * per bin in LDS, claims one range per touched bin with a single global
- * atomic, then writes perm[].  Order inside a bin is unspecified; digests
- * are stored by packet index, so the output does not depend on it.
- */
-__global__ __launch_bounds__(256) void bin_scatter_kernel(
-    const uint32_t *__restrict__ lens, uint64_t n, int blk_shift,
-    int lenbytes, const uint32_t *__restrict__ hist,
-    uint32_t *__restrict__ cursor, uint32_t *__restrict__ perm)
-{
-	__shared__ uint32_t cnt[NET2_SHA2_NBINS];
-	__shared__ uint32_t basep[NET2_SHA2_NBINS];
-	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
-		cnt[b] = 0;
-	if (NET2_BIN_FUSED)
-		hist_prefix_lds(hist, basep);
-	__syncthreads();
-	const uint64_t i0 = (uint64_t)blockIdx.x * NET2_BIN_TILE + threadIdx.x;
-	uint32_t bin[NET2_BIN_ITEMS], rank[NET2_BIN_ITEMS];
-	load_lens(lens, n, i0, bin);
-#pragma unroll
-	for (int k = 0; k < NET2_BIN_ITEMS; k++) {
-		const bool live = i0 + (uint64_t)k * 256 < n;
-		bin[k] = live ? bin_of(bin[k], blk_shift, lenbytes,
-		    NET2_SHA2_NBINS) : 0;
-		rank[k] = wave_rank_add(cnt, bin[k], live);
-	}
-	__syncthreads();
-	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
-		if (cnt[b] != 0)
-			basep[b] = (NET2_BIN_FUSED ? basep[b] : 0) +
-			    atomicAdd(&cursor[b], cnt[b]);
-	__syncthreads();
-#pragma unroll
-	for (int k = 0; k < NET2_BIN_ITEMS; k++) {
-		const uint64_t i = i0 + (uint64_t)k * 256;
-		if (i < n)
-			perm[basep[bin[k]] + rank[k]] = (uint32_t)i;
-	}
-}
-
-/*
- * One-pass binning (NET2_BIN_ONEPASS): the count, the global prefix and the
- * scatter in one launch, no memset.  A persistent grid of G <= 256
+ * Binning in one launch (round 4; until round 3 a memset, a count and a
+ * scatter launch): the count, the global prefix and the scatter, no memset.  A persistent grid of G <= 256
  * workgroups (each loops over its 4,096-packet tiles):
  *   1. LDS histogram of its tiles, each packet's rank in its bin kept in
  *      registers (the LDS atomic's return value), then one device-scope
@@ -2063,20 +1885,13 @@ __global__ __launch_bounds__(256) void bin_scatter_kernel(
  * Memory ordering.  What crosses the barrier is the histogram, written and
  * read only by device-scope atomics, each workgroup's adds returned before
  * it arrives; the plain stores (perm, the next parity's zeroes) are read
- * only by later launches.  So the barrier needs no cache maintenance
- * (NET2_BIN_FENCE=0, shipped).  On gfx950 an agent-scope release writes back
- * the XCD's L2 and an acquire invalidates it; with acq_rel arrivals and an
- * acquire fence (1) the launch measured ~15 % longer, with an acquiring
- * load per poll (2) ~3x (profiles/round4/bin_probe_*.txt).
+ * only by later launches.  So the barrier needs no cache maintenance: its
+ * atomics are relaxed.  On gfx950 an agent-scope release writes back the
+ * XCD's L2 and an acquire invalidates it; with acq_rel arrivals and an
+ * acquire fence the launch measured ~15 % longer, with an acquiring load
+ * per poll ~3x (profiles/round4/bin_probe_*.txt).
  */
-#ifndef NET2_BIN_ONEPASS
-#define NET2_BIN_ONEPASS 1
-#endif
-#ifndef NET2_BIN_FENCE
-#define NET2_BIN_FENCE 0
-#endif
-#define BIN_ORD (NET2_BIN_FENCE >= 1 ? __ATOMIC_ACQ_REL : __ATOMIC_RELAXED)
-#define BIN_ACQ (NET2_BIN_FENCE >= 1 ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED)
+#define BIN_ORD __ATOMIC_RELAXED
 #ifndef NET2_BIN_SPIN_SLEEP
 #define NET2_BIN_SPIN_SLEEP 2
 #endif
@@ -2154,7 +1969,7 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 	load_lens(lens, n, (uint64_t)blockIdx.x * NET2_BIN_TILE + threadIdx.x,
 	    len);
 	if (threadIdx.x == 0) {
-		bc[0] = __hip_atomic_load(&h->magic, BIN_ACQ,
+		bc[0] = __hip_atomic_load(&h->magic, __ATOMIC_RELAXED,
 		    __HIP_MEMORY_SCOPE_AGENT) == NET2_BIN_MAGIC;
 		bc[1] = ld_agent(&h->epoch);
 	}
@@ -2239,7 +2054,7 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 			    __HIP_MEMORY_SCOPE_AGENT);
 			uint32_t exp = BIN_UNDECIDED;
 			__hip_atomic_compare_exchange_strong(&ctl[BIN_CTL_STATE],
-			    &exp, (uint32_t)BIN_GO, BIN_ORD, BIN_ACQ,
+			    &exp, (uint32_t)BIN_GO, BIN_ORD, __ATOMIC_RELAXED,
 			    __HIP_MEMORY_SCOPE_AGENT);
 		}
 		BIN_STAMP(3);
@@ -2250,13 +2065,11 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 				uint32_t exp = BIN_UNDECIDED;
 				__hip_atomic_compare_exchange_strong(
 				    &ctl[BIN_CTL_STATE], &exp,
-				    (uint32_t)BIN_ABORT, BIN_ORD, BIN_ACQ,
+				    (uint32_t)BIN_ABORT, BIN_ORD, __ATOMIC_RELAXED,
 				    __HIP_MEMORY_SCOPE_AGENT);
 			}
 			__builtin_amdgcn_s_sleep(NET2_BIN_SPIN_SLEEP);
 		}
-		if (NET2_BIN_FENCE >= 1)
-			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 		BIN_STAMP(4);
 		bc[0] = st;
 	}
@@ -2349,85 +2162,6 @@ __global__ __launch_bounds__(256) void bin_ws_init_kernel(uint32_t *ws)
 	if (threadIdx.x == 0)
 		__hip_atomic_store(&h->magic, NET2_BIN_MAGIC, __ATOMIC_RELEASE,
 		    __HIP_MEMORY_SCOPE_AGENT);
-}
-
-/*
- * Tile-local binning (NET2_BIN_TILESORT=1; measured and NOT the default):
- * one launch, no global histogram -- workgroup t counting-sorts its own
- * tile of NET2_BIN_TILE_SORT packets by descending block count in LDS.
- * Waves stay length-uniform, the binning itself takes 10 us instead of
- * ~16 us plus a memset and a launch gap, yet the hash kernel runs 2x
- * slower (C3: 904 us against 442 us, profiles/round2/binning_tile_ab.txt):
- * the global order is also a longest-first schedule.  A wave of 1,500-byte
- * packets lives ~170 us at 3 waves per SIMD; dispatched first, the long
- * waves finish while short ones fill in behind them, whereas tile order
- * keeps starting long waves until the very end of the grid.
- */
-#ifndef NET2_BIN_TILESORT
-#define NET2_BIN_TILESORT 0
-#endif
-#ifndef NET2_BIN_SORT_ITEMS
-#define NET2_BIN_SORT_ITEMS 32
-#endif
-#define NET2_BIN_TILE_SORT (256 * NET2_BIN_SORT_ITEMS)
-
-__global__ __launch_bounds__(256) void bin_tile_kernel(
-    const uint32_t *__restrict__ lens, uint64_t n, int blk_shift,
-    int lenbytes, uint32_t *__restrict__ perm)
-{
-	__shared__ uint32_t cnt[NET2_SHA2_NBINS];
-	__shared__ uint32_t wsum[4];
-	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
-		cnt[b] = 0;
-	__syncthreads();
-	const uint64_t t0 = (uint64_t)blockIdx.x * NET2_BIN_TILE_SORT;
-	uint32_t bin[NET2_BIN_SORT_ITEMS], rank[NET2_BIN_SORT_ITEMS];
-#pragma unroll
-	for (int k = 0; k < NET2_BIN_SORT_ITEMS; k++) {
-		const uint64_t i = t0 + (uint64_t)k * 256 + threadIdx.x;
-		bin[k] = i < n ? lens[i] : 0u;
-	}
-#pragma unroll
-	for (int k = 0; k < NET2_BIN_SORT_ITEMS; k++) {
-		const bool live = t0 + (uint64_t)k * 256 + threadIdx.x < n;
-		bin[k] = live ? bin_of(bin[k], blk_shift, lenbytes,
-		    NET2_SHA2_NBINS) : 0;
-		rank[k] = live ? atomicAdd(&cnt[bin[k]], 1u) : 0u;
-	}
-	__syncthreads();
-	/* exclusive scan of the tile histogram: 8 bins per thread, a shuffle
-	 * scan per wave, the four wave totals */
-	constexpr int PER = NET2_SHA2_NBINS / 256;
-	const int lane = (int)__lane_id(), wave = (int)(threadIdx.x / 64);
-	uint32_t v[PER], sum = 0;
-#pragma unroll
-	for (int j = 0; j < PER; j++) {
-		v[j] = sum;
-		sum += cnt[threadIdx.x * PER + j];
-	}
-	uint32_t x = sum;
-#pragma unroll
-	for (int off = 1; off < 64; off <<= 1) {
-		const uint32_t y = __shfl_up(x, off);
-		if (lane >= off)
-			x += y;
-	}
-	if (lane == 63)
-		wsum[wave] = x;
-	__syncthreads();
-	uint32_t base = x - sum;
-	for (int w = 0; w < wave; w++)
-		base += wsum[w];
-#pragma unroll
-	for (int j = 0; j < PER; j++)
-		cnt[threadIdx.x * PER + j] = base + v[j];
-	__syncthreads();
-#pragma unroll
-	for (int k = 0; k < NET2_BIN_SORT_ITEMS; k++) {
-		const uint64_t i = t0 + (uint64_t)k * 256 + threadIdx.x;
-		if (i < n)
-			perm[t0 + cnt[bin[k]] + rank[k]] = (uint32_t)i;
-	}
 }
 
 /* ---- host-side constant pad schedule ---------------------------------- */
@@ -2531,8 +2265,7 @@ hipError_t net2_launch_fixed(int alg, const uint8_t *base, uint64_t stride,
 
 hipError_t net2_bin_ws_init(uint32_t *ws, hipStream_t s)
 {
-	if (NET2_BIN_ONEPASS)
-		bin_ws_init_kernel<<<1, 256, 0, s>>>(ws);
+	bin_ws_init_kernel<<<1, 256, 0, s>>>(ws);
 	return hipGetLastError();
 }
 
@@ -2543,40 +2276,16 @@ hipError_t net2_bin_order(int alg, const uint32_t *lens, uint64_t n,
 	const bool s256 = alg == NET2_ALG_SHA256;
 	const int blk_shift = s256 ? 6 : 7;
 	const int lenbytes = s256 ? 8 : 16;
-	uint32_t *hist = ws + NET2_BIN_HDR;
-	uint32_t *cursor = hist + NET2_SHA2_NBINS;
-	uint32_t *perm = ws + NET2_BIN_WS_WORDS;
-	if (NET2_BIN_TILESORT) {
-		const unsigned g = (unsigned)((n + NET2_BIN_TILE_SORT - 1) /
-		    NET2_BIN_TILE_SORT);
-		bin_tile_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift, lenbytes,
-		    perm);
-		return hipGetLastError();
-	}
-	if (NET2_BIN_ONEPASS) {
-		const uint64_t tiles = (n + NET2_BIN_TILE - 1) / NET2_BIN_TILE;
-		const unsigned g = (unsigned)(tiles < NET2_BIN_GRID ? tiles :
-		    NET2_BIN_GRID);
-		/* NET2_BIN_TIMEOUT_US (tests): the barrier's timeout, default
-		 * 50 ms; 0 exercises the ABORT path */
-		const char *e = getenv("NET2_BIN_TIMEOUT_US");
-		const uint64_t to = e != nullptr && *e != '\0' ?
-		    strtoull(e, nullptr, 10) * 100 : NET2_BIN_TIMEOUT;
-		bin_onepass_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift,
-		    lenbytes, ws, to);
-		return hipGetLastError();
-	}
-	/* fused: cursor holds per-bin claim counters, zeroed with hist */
-	hipError_t e = hipMemsetAsync(hist, 0, (NET2_BIN_FUSED ? 2 : 1) *
-	    NET2_SHA2_NBINS * sizeof(uint32_t), s);
-	if (e != hipSuccess)
-		return e;
-	const unsigned g = (unsigned)((n + NET2_BIN_TILE - 1) / NET2_BIN_TILE);
-	bin_count_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift, lenbytes, hist);
-	if (!NET2_BIN_FUSED)
-		bin_scan_kernel<<<1, 1024, 0, s>>>(hist, cursor);
-	bin_scatter_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift, lenbytes, hist,
-	    cursor, perm);
+	const uint64_t tiles = (n + NET2_BIN_TILE - 1) / NET2_BIN_TILE;
+	const unsigned g = (unsigned)(tiles < NET2_BIN_GRID ? tiles :
+	    NET2_BIN_GRID);
+	/* NET2_BIN_TIMEOUT_US (tests): the barrier's timeout, default 50 ms;
+	 * 0 exercises the ABORT path */
+	const char *e = getenv("NET2_BIN_TIMEOUT_US");
+	const uint64_t to = e != nullptr && *e != '\0' ?
+	    strtoull(e, nullptr, 10) * 100 : NET2_BIN_TIMEOUT;
+	bin_onepass_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift, lenbytes, ws,
+	    to);
 	return hipGetLastError();
 }
 
