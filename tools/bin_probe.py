@@ -44,8 +44,9 @@ def main():
         base = 16 + 2 * nb + 2048          # after the histograms, barrier words
         st = ws.cpu().numpy().view(np.uint32)[base:base + 256 * 8]
         st = st.reshape(256, 8).astype(np.int64)
+        st = st[st[:, 0] != 0]            # the grid's workgroups (G <= 256)
         st = (st - st[:, 0].min()) & 0xffffffff
-        print(f"== {name}: {n} packets, 256 workgroups (us from first start)")
+        print(f"== {name}: {n} packets, {len(st)} workgroups (us from first start)")
         names = ["start", "counted", "hist added", "arrived", "decided",
                  "bases", "perm written"]
         for p in range(7):
