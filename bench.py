@@ -806,6 +806,13 @@ def extra_configs(args, dev, probe, ws=1, rank=0, label=None):
         if rank == 0 and not args.no_cpu_baseline:
             out[name]["cpu_baseline"] = cpu_baseline(CONFIGS[name], light=True)
     out["e2e"] = e2e_rate(steps=10, warmup=3)
+    # the per-datagram path from host memory (north_star: "starts and ends
+    # in host memory"), pinned buffers; the pageable rate beside it
+    for kind in ("rx", "tx"):
+        r = burst_e2e_rate(kind)
+        pg = burst_e2e_rate(kind, steps=4, warmup=1, memory="pageable")
+        r["pageable"] = {k: pg[k] for k in ("value", "ms_per_step", "h2d_GBps")}
+        out[f"burst_{kind}_e2e"] = r
     out["c1"] = run_c1()
     return out
 
@@ -904,6 +911,79 @@ def _e2e_timed(steps, warmup, n, length, ws, dev, dist_backend, numa,
                         "one rank per GPU (BASELINE configs[4] at N=8)",
             "h2d_GBps_per_gpu": round(n * length / (ms / 1e3) / 1e9, 2),
             "host_buffers_numa_local": numa}
+
+
+def burst_e2e_rate(kind, steps=8, warmup=2, n=1 << 20, memory="pinned"):
+    """The burst configs end to end from host memory (VERDICT round 4 item
+    1): 1 M wire datagrams of {136, 584, 1500} B (8-byte header, 64-byte
+    HMAC-SHA512 field, payload; every one PH_SIGNED|PH_ENCRYPTED) in host
+    memory -> net2_packet_decode_burst_host (RX: codes, headers and 16-byte
+    IVs back to host memory) or net2_packet_encode_burst_host (TX: header
+    and HMAC field sealed into the caller's buffer) on this process's GPU
+    (max_devices 1).  The datagrams are sealed once, untimed, before the RX
+    steps."""
+    import numpy as np
+    import torch
+    from ilias_net2_amd import _lib
+    import ctypes
+    L = _lib.lib()
+    rng = np.random.default_rng(7)
+    lens = rng.choice(np.array([136, 584, 1500], dtype=np.uint32), n)
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    total = int(lens.sum())
+    seq = np.arange(n, dtype=np.uint32)
+    flags = np.full(n, 3, dtype=np.uint32)
+    key = HMAC_KEY[:64]
+
+    def host(shape, dt):
+        if memory == "pinned":
+            t = torch.empty(shape, dtype={np.uint8: torch.uint8,
+                                          np.uint32: torch.int32}[dt], pin_memory=True)
+            return t.numpy().view(dt)
+        return np.empty(shape, dtype=dt)
+    data = host((total,), np.uint8)
+    data[:] = rng.integers(0, 256, total, dtype=np.uint8)
+    res = host((n,), np.uint8)
+    p = lambda a: a.ctypes.data  # noqa: E731
+
+    def tx():
+        _lib.check(L.net2_packet_encode_burst_host(
+            6, key, 64, 1, p(seq), p(flags), p(data), p(offs), p(lens), n,
+            p(res), 1), "net2_packet_encode_burst_host")
+    iv = host((n, 16), np.uint8)
+    oseq, ofl = host((n,), np.uint32), host((n,), np.uint32)
+    kb = ctypes.create_string_buffer(key, 64)
+    keys = _lib.BurstRxKeys(6, ctypes.cast(kb, ctypes.c_void_p), 64, 1, None, 0, 0, 0, 0)
+
+    def rx():
+        _lib.check(L.net2_packet_decode_burst_host(
+            ctypes.byref(keys), 16, p(data), p(offs), p(lens), n, p(res), p(iv),
+            p(oseq), p(ofl), 1), "net2_packet_decode_burst_host")
+    tx()
+    assert int((res != 0).sum()) == 0, "burst seal failed"
+    step = rx if kind == "rx" else tx
+    for _ in range(warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    ms = (time.perf_counter() - t0) * 1e3 / steps
+    assert int((res != 0).sum()) == 0, f"burst {kind}: datagrams not OK"
+    out_bytes = n * (1 + 16 + 8) if kind == "rx" else n * (1 + 8 + 64)
+    r = {"metric": ("datagrams decoded/s" if kind == "rx" else "datagrams encoded/s") +
+                   f", 1M x {{136,584,1500}} B wire datagrams from {memory} host memory, "
+                   "end to end (pack, H2D, HMAC-SHA512" +
+                   (" verify + 16-B IVs" if kind == "rx" else " seal") +
+                   ", results to host memory), 1 GPU",
+         "value": round(n / (ms / 1e3), 1), "unit": "datagrams/s", "steps": steps,
+         "ms_per_step": round(ms, 3),
+         "workload": f"net2_packet_{'decode' if kind == 'rx' else 'encode'}_burst_host, "
+                     f"{memory} datagram buffer and result arrays, max_devices 1",
+         "h2d_GBps": round(total / (ms / 1e3) / 1e9, 2),
+         "host_bytes_per_step": {"datagrams_in": total, "results_out": out_bytes}}
+    del data, res, iv, oseq, ofl
+    return r
 
 
 def run_c1():

@@ -42,6 +42,13 @@ class BurstRxKeys(ctypes.Structure):
                 ("rx_start", ctypes.c_uint32)]
 
 
+class BinStats(ctypes.Structure):
+    """struct net2_bin_stats (include/net2/sha2_batch.h)."""
+    _fields_ = [("prepared", ctypes.c_uint32), ("binned", ctypes.c_uint32),
+                ("aborts", ctypes.c_uint32), ("mismatches", ctypes.c_uint32),
+                ("unprepared", ctypes.c_uint32)]
+
+
 _c_u64p = ctypes.POINTER(ctypes.c_uint64)
 _c_u32p = ctypes.POINTER(ctypes.c_uint32)
 
@@ -64,6 +71,9 @@ SIGNATURES = {
     "net2_sha2_dev_var_workspace": (ctypes.c_size_t, [ctypes.c_uint64]),
     "net2_sha2_workspace_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t,
                                                 ctypes.c_void_p]),
+    "net2_sha2_workspace_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t,
+                                                 ctypes.c_void_p]),
+    "net2_sha2_bin_limits": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_int64]),
     "net2_sha2_batch": (ctypes.c_int, [
         ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
         ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
@@ -113,6 +123,14 @@ SIGNATURES = {
         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
         ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
         ctypes.c_size_t, ctypes.c_void_p]),
+    "net2_packet_decode_burst_host": (ctypes.c_int, [
+        ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "net2_packet_encode_burst_host": (ctypes.c_int, [
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]),
     # include/net2/sha2.h: the streaming interface of src/sha2.c
     "net2_sha2_ctx_init": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p]),
     "net2_sha2_ctx_update": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p,
@@ -184,6 +202,14 @@ def check(rc: int, what: str = "") -> None:
 
 def hashmax() -> int:
     return ctypes.c_int.in_dll(lib(), "net2_hashmax").value
+
+
+def workspace_stats(ws_ptr: int, ws_bytes: int) -> dict:
+    """net2_sha2_workspace_stats of a device workspace, as a dict."""
+    st = BinStats()
+    check(lib().net2_sha2_workspace_stats(ws_ptr, ws_bytes, ctypes.byref(st)),
+          "net2_sha2_workspace_stats")
+    return {f: getattr(st, f) for f, _ in BinStats._fields_}
 
 
 def device_count() -> int:

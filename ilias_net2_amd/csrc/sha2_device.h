@@ -148,7 +148,7 @@ __device__ __forceinline__ uint32_t ssig1_256(uint32_t x)
  * caller passes K and W separately.
  */
 /*
- * NET2_ASM256 = 1: the body of a round (and of a schedule word) is one
+ * Ordered asm rounds (ASM = true, every kernel): the body of a round (and of a schedule word) is one
  * inline-asm block with a fixed instruction order: the six rotates of e and
  * a are independent of each other and are issued back to back, Ch/Maj and
  * the Sigma xors fill in between, the adds come last.  Left to itself the
@@ -159,14 +159,11 @@ __device__ __forceinline__ uint32_t ssig1_256(uint32_t x)
  * multiset, only the order differs).  h + K + W stays outside the block so
  * the compiler can take K (or the pad block's K + W) from an SGPR.
  */
-#ifndef NET2_ASM256
-#define NET2_ASM256 1
-#endif
-#ifndef NET2_FENCE256
-#define NET2_FENCE256 2
-#endif
+constexpr bool kAsm256 = true;
+/* a scheduling fence every 2 rounds (see Rounds256) */
+constexpr int kFence256 = 2;
 
-/* The round body as one asm block (see NET2_ASM256). */
+/* The round body as one asm block (see above). */
 __device__ __forceinline__ void round256_asm(uint32_t a, uint32_t b,
     uint32_t c, uint32_t &d, uint32_t e, uint32_t f, uint32_t g,
     uint32_t &h, uint32_t x)
@@ -191,7 +188,7 @@ __device__ __forceinline__ void round256_asm(uint32_t a, uint32_t b,
 	      [g] "v"(g), [x] "v"(x));
 }
 
-template <int T, bool ASM = NET2_ASM256>
+template <int T, bool ASM = kAsm256>
 __device__ __forceinline__ void round256(uint32_t (&s)[8], uint32_t k,
     uint32_t w)
 {
@@ -207,7 +204,7 @@ __device__ __forceinline__ void round256(uint32_t (&s)[8], uint32_t k,
 	}
 }
 
-/* sigma1(y) + w7 + sigma0(x) + w16 as one asm block (see NET2_ASM256). */
+/* sigma1(y) + w7 + sigma0(x) + w16 as one asm block (see round256_asm). */
 __device__ __forceinline__ void expand256_asm(uint32_t &w16, uint32_t w7,
     uint32_t x, uint32_t y)
 {
@@ -228,7 +225,7 @@ __device__ __forceinline__ void expand256_asm(uint32_t &w16, uint32_t w7,
 }
 
 /* W[t & 15] for t >= 16, in place over the 16-word circular schedule. */
-template <int T, bool ASM = NET2_ASM256>
+template <int T, bool ASM = kAsm256>
 __device__ __forceinline__ uint32_t expand256(uint32_t (&w)[16])
 {
 	if (ASM)
@@ -249,7 +246,7 @@ struct Rounds256 {
 		round256<T, ASM>(s, K256[T], wt);
 		/* keep the schedule words from being computed far ahead of
 		 * their rounds (register pressure: 8 waves/SIMD need <= 64) */
-		if (ASM && NET2_FENCE256 > 0 && T % NET2_FENCE256 == NET2_FENCE256 - 1)
+		if (ASM && kFence256 > 0 && T % kFence256 == kFence256 - 1)
 			__builtin_amdgcn_sched_barrier(0);
 		Rounds256<T + 1, ASM>::run(s, w);
 	}
@@ -261,7 +258,7 @@ struct Rounds256<64, ASM> {
 };
 
 /* SHA256Transform (src/sha2.c:374-445) on registers: st += F(st, w). */
-template <bool ASM = NET2_ASM256>
+template <bool ASM = kAsm256>
 __device__ __forceinline__ void compress256(uint32_t (&st)[8],
     uint32_t (&w)[16])
 {
@@ -287,7 +284,7 @@ struct RoundsKW256 {
 	    const uint32_t *kw)
 	{
 		round256<T, ASM>(s, kw[T], 0u);
-		if (ASM && NET2_FENCE256 > 0 && T % NET2_FENCE256 == NET2_FENCE256 - 1)
+		if (ASM && kFence256 > 0 && T % kFence256 == kFence256 - 1)
 			__builtin_amdgcn_sched_barrier(0);
 		RoundsKW256<T + 1, ASM>::run(s, kw);
 	}
@@ -298,7 +295,7 @@ struct RoundsKW256<64, ASM> {
 	    const uint32_t *) {}
 };
 
-template <bool ASM = NET2_ASM256>
+template <bool ASM = kAsm256>
 __device__ __forceinline__ void compress256_kw(uint32_t (&st)[8],
     const uint32_t *kw)
 {
@@ -385,22 +382,14 @@ __device__ __forceinline__ uint64_t bsig1_512(uint64_t e)
  * v_alignbit_b32 + v_lshrrev_b32, two VALU ops for the same result).
  * Issue costs (tools/valu_probe): v_lshrrev_b64 4.2 SIMD cycles per wave
  * instruction against 4.3 + 2.6 for the pair; measured -2% on the SHA-512
- * fixed kernel (profiles/round1/sha512_u2_shr_ab.json).  NET2_SHR64_ASM=0
- * restores the plain C shift.
+ * fixed kernel (profiles/round1/sha512_u2_shr_ab.json).
  */
-#ifndef NET2_SHR64_ASM
-#define NET2_SHR64_ASM 1
-#endif
 template <int N>
 __device__ __forceinline__ uint64_t shr64(uint64_t x)
 {
-#if NET2_SHR64_ASM
 	uint64_t r;
 	asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(N), "v"(x));
 	return r;
-#else
-	return x >> N;
-#endif
 }
 
 __device__ __forceinline__ uint64_t ssig0_512(uint64_t x)
@@ -413,105 +402,22 @@ __device__ __forceinline__ uint64_t ssig1_512(uint64_t x)
 }
 
 /*
- * NET2_ASM512 = 1: the bitwise half of a SHA-512 round -- the 12 rotates of
- * Sigma1(e) and Sigma0(a) (two v_alignbit_b32 per 64-bit rotate) and the 8
- * v_bitop3_b32 of the Sigma xors, Ch and Maj -- as one asm block with a
- * fixed order (rotates first), as NET2_ASM256 does for SHA-256; the 64-bit
- * sums stay in C (v_lshl_add_u64 needs register pairs, which inline asm
- * cannot split into halves).
+ * The bitwise half of a SHA-512 round -- the 12 rotates of Sigma1(e) and
+ * Sigma0(a) (two v_alignbit_b32 per 64-bit rotate) and the 8 v_bitop3_b32 of
+ * the Sigma xors, Ch and Maj -- as one asm block with a fixed order (rotates
+ * first), as round256_asm does for SHA-256; the 64-bit sums stay in C
+ * (v_lshl_add_u64 needs register pairs, which inline asm cannot split into
+ * halves).  Three other orders measured within 1 % on C4, c3_512 and
+ * hmac512_mtu (profiles/round2/sha512_order_ab.txt) and were removed.
  */
-#ifndef NET2_ASM512
-#define NET2_ASM512 1
-#endif
-#ifndef NET2_ORD512	/* instruction order of the round's asm block */
-#define NET2_ORD512 0
-#endif
-/* orders 1 and 2 keep Sigma1's rotates live while Sigma0's are made */
-#if NET2_ORD512 == 1 || NET2_ORD512 == 2
-#define NET2_Q512_OUTS [q1] "=&v"(q1), [q2] "=&v"(q2), [q3] "=&v"(q3), \
-	[q4] "=&v"(q4), [q5] "=&v"(q5), [q6] "=&v"(q6),
-#else
-#define NET2_Q512_OUTS
-#endif
-#ifndef NET2_ASM512X	/* the schedule words too */
-#define NET2_ASM512X NET2_ASM512
-#endif
-
 __device__ __forceinline__ void bitwise512_asm(uint64_t a, uint64_t b,
     uint64_t c, uint64_t e, uint64_t f, uint64_t g, uint64_t &S1,
     uint64_t &CH, uint64_t &S0, uint64_t &MJ)
 {
 	uint32_t r1, r2, r3, r4, r5, r6;
-#if NET2_ORD512 == 1 || NET2_ORD512 == 2
-	uint32_t q1, q2, q3, q4, q5, q6;
-#endif
 	uint32_t s1l, s1h, chl, chh, s0l, s0h, mjl, mjh;
 	/* rotr n < 32: lo = alignbit(hi, lo, n), hi = alignbit(lo, hi, n);
 	 * rotr 32 + m: lo = alignbit(lo, hi, m), hi = alignbit(hi, lo, m) */
-#if NET2_ORD512 == 1
-	asm("v_bitop3_b32 %[chl], %[el], %[fl], %[gl] bitop3:0xca\n\t"
-	    "v_bitop3_b32 %[chh], %[eh], %[fh], %[gh] bitop3:0xca\n\t"
-	    "v_bitop3_b32 %[mjl], %[al], %[bl], %[cl] bitop3:0xe8\n\t"
-	    "v_bitop3_b32 %[mjh], %[ah], %[bh], %[ch] bitop3:0xe8\n\t"
-	    "v_alignbit_b32 %[r1], %[eh], %[el], 14\n\t"
-	    "v_alignbit_b32 %[r2], %[eh], %[el], 18\n\t"
-	    "v_alignbit_b32 %[r3], %[el], %[eh], 9\n\t"
-	    "v_alignbit_b32 %[r4], %[el], %[eh], 14\n\t"
-	    "v_alignbit_b32 %[r5], %[el], %[eh], 18\n\t"
-	    "v_alignbit_b32 %[r6], %[eh], %[el], 9\n\t"
-	    "v_alignbit_b32 %[q1], %[ah], %[al], 28\n\t"
-	    "v_alignbit_b32 %[q2], %[al], %[ah], 2\n\t"
-	    "v_alignbit_b32 %[q3], %[al], %[ah], 7\n\t"
-	    "v_alignbit_b32 %[q4], %[al], %[ah], 28\n\t"
-	    "v_alignbit_b32 %[q5], %[ah], %[al], 2\n\t"
-	    "v_alignbit_b32 %[q6], %[ah], %[al], 7\n\t"
-	    "v_bitop3_b32 %[s1l], %[r1], %[r2], %[r3] bitop3:0x96\n\t"
-	    "v_bitop3_b32 %[s1h], %[r4], %[r5], %[r6] bitop3:0x96\n\t"
-	    "v_bitop3_b32 %[s0l], %[q1], %[q2], %[q3] bitop3:0x96\n\t"
-	    "v_bitop3_b32 %[s0h], %[q4], %[q5], %[q6] bitop3:0x96"
-#elif NET2_ORD512 == 2
-	asm("v_alignbit_b32 %[r1], %[eh], %[el], 14\n\t"
-	    "v_alignbit_b32 %[r2], %[eh], %[el], 18\n\t"
-	    "v_alignbit_b32 %[r3], %[el], %[eh], 9\n\t"
-	    "v_alignbit_b32 %[r4], %[el], %[eh], 14\n\t"
-	    "v_alignbit_b32 %[r5], %[el], %[eh], 18\n\t"
-	    "v_alignbit_b32 %[r6], %[eh], %[el], 9\n\t"
-	    "v_alignbit_b32 %[q1], %[ah], %[al], 28\n\t"
-	    "v_alignbit_b32 %[q2], %[al], %[ah], 2\n\t"
-	    "v_alignbit_b32 %[q3], %[al], %[ah], 7\n\t"
-	    "v_alignbit_b32 %[q4], %[al], %[ah], 28\n\t"
-	    "v_alignbit_b32 %[q5], %[ah], %[al], 2\n\t"
-	    "v_alignbit_b32 %[q6], %[ah], %[al], 7\n\t"
-	    "v_bitop3_b32 %[s1l], %[r1], %[r2], %[r3] bitop3:0x96\n\t"
-	    "v_bitop3_b32 %[s1h], %[r4], %[r5], %[r6] bitop3:0x96\n\t"
-	    "v_bitop3_b32 %[chl], %[el], %[fl], %[gl] bitop3:0xca\n\t"
-	    "v_bitop3_b32 %[chh], %[eh], %[fh], %[gh] bitop3:0xca\n\t"
-	    "v_bitop3_b32 %[s0l], %[q1], %[q2], %[q3] bitop3:0x96\n\t"
-	    "v_bitop3_b32 %[s0h], %[q4], %[q5], %[q6] bitop3:0x96\n\t"
-	    "v_bitop3_b32 %[mjl], %[al], %[bl], %[cl] bitop3:0xe8\n\t"
-	    "v_bitop3_b32 %[mjh], %[ah], %[bh], %[ch] bitop3:0xe8"
-#elif NET2_ORD512 == 3
-	asm("v_alignbit_b32 %[r1], %[eh], %[el], 14\n\t"
-	    "v_alignbit_b32 %[r2], %[eh], %[el], 18\n\t"
-	    "v_alignbit_b32 %[r3], %[el], %[eh], 9\n\t"
-	    "v_bitop3_b32 %[s1l], %[r1], %[r2], %[r3] bitop3:0x96\n\t"
-	    "v_alignbit_b32 %[r4], %[el], %[eh], 14\n\t"
-	    "v_alignbit_b32 %[r5], %[el], %[eh], 18\n\t"
-	    "v_alignbit_b32 %[r6], %[eh], %[el], 9\n\t"
-	    "v_bitop3_b32 %[s1h], %[r4], %[r5], %[r6] bitop3:0x96\n\t"
-	    "v_bitop3_b32 %[chl], %[el], %[fl], %[gl] bitop3:0xca\n\t"
-	    "v_bitop3_b32 %[chh], %[eh], %[fh], %[gh] bitop3:0xca\n\t"
-	    "v_alignbit_b32 %[r1], %[ah], %[al], 28\n\t"
-	    "v_alignbit_b32 %[r2], %[al], %[ah], 2\n\t"
-	    "v_alignbit_b32 %[r3], %[al], %[ah], 7\n\t"
-	    "v_bitop3_b32 %[s0l], %[r1], %[r2], %[r3] bitop3:0x96\n\t"
-	    "v_alignbit_b32 %[r4], %[al], %[ah], 28\n\t"
-	    "v_alignbit_b32 %[r5], %[ah], %[al], 2\n\t"
-	    "v_alignbit_b32 %[r6], %[ah], %[al], 7\n\t"
-	    "v_bitop3_b32 %[s0h], %[r4], %[r5], %[r6] bitop3:0x96\n\t"
-	    "v_bitop3_b32 %[mjl], %[al], %[bl], %[cl] bitop3:0xe8\n\t"
-	    "v_bitop3_b32 %[mjh], %[ah], %[bh], %[ch] bitop3:0xe8"
-#else
 	asm("v_alignbit_b32 %[r1], %[eh], %[el], 14\n\t"
 	    "v_alignbit_b32 %[r2], %[eh], %[el], 18\n\t"
 	    "v_alignbit_b32 %[r3], %[el], %[eh], 9\n\t"
@@ -532,9 +438,8 @@ __device__ __forceinline__ void bitwise512_asm(uint64_t a, uint64_t b,
 	    "v_bitop3_b32 %[s0h], %[r4], %[r5], %[r6] bitop3:0x96\n\t"
 	    "v_bitop3_b32 %[mjl], %[al], %[bl], %[cl] bitop3:0xe8\n\t"
 	    "v_bitop3_b32 %[mjh], %[ah], %[bh], %[ch] bitop3:0xe8"
-#endif
 	    : [r1] "=&v"(r1), [r2] "=&v"(r2), [r3] "=&v"(r3), [r4] "=&v"(r4),
-	      [r5] "=&v"(r5), [r6] "=&v"(r6), NET2_Q512_OUTS
+	      [r5] "=&v"(r5), [r6] "=&v"(r6),
 	      [s1l] "=&v"(s1l), [s1h] "=&v"(s1h),
 	      [chl] "=&v"(chl), [chh] "=&v"(chh), [s0l] "=&v"(s0l),
 	      [s0h] "=&v"(s0h), [mjl] "=&v"(mjl), [mjh] "=&v"(mjh)
@@ -554,22 +459,16 @@ __device__ __forceinline__ void round512(uint64_t (&s)[8], uint64_t kw)
 	uint64_t &a = s[(0 - T) & 7], &b = s[(1 - T) & 7], &c = s[(2 - T) & 7];
 	uint64_t &d = s[(3 - T) & 7], &e = s[(4 - T) & 7], &f = s[(5 - T) & 7];
 	uint64_t &g = s[(6 - T) & 7], &h = s[(7 - T) & 7];
-	if (NET2_ASM512) {
-		uint64_t S1, CH, S0, MJ;
-		bitwise512_asm(a, b, c, e, f, g, S1, CH, S0, MJ);
-		uint64_t t1 = h + kw + S1 + CH;
-		d += t1;
-		h = t1 + S0 + MJ;
-		return;
-	}
-	uint64_t t1 = h + kw + bsig1_512(e) + ch64(e, f, g);
+	uint64_t S1, CH, S0, MJ;
+	bitwise512_asm(a, b, c, e, f, g, S1, CH, S0, MJ);
+	uint64_t t1 = h + kw + S1 + CH;
 	d += t1;
-	h = t1 + bsig0_512(a) + maj64(a, b, c);
+	h = t1 + S0 + MJ;
 }
 
 /*
  * sigma0(x) and sigma1(y) of a SHA-512 schedule word with the rotates in one
- * ordered asm block (NET2_ASM512); the 64-bit shifts (v_lshrrev_b64) are
+ * ordered asm block (as bitwise512_asm); the 64-bit shifts (v_lshrrev_b64) are
  * passed in, their halves read directly.
  */
 __device__ __forceinline__ void ssigmas512_asm(uint64_t x, uint64_t y,
@@ -601,41 +500,27 @@ __device__ __forceinline__ void ssigmas512_asm(uint64_t x, uint64_t y,
 template <int T>
 __device__ __forceinline__ uint64_t expand512(uint64_t (&w)[16])
 {
-	if (NET2_ASM512X) {
-		const uint64_t x = w[(T - 15) & 15], y = w[(T - 2) & 15];
-		uint64_t P0, P1;
-		ssigmas512_asm(x, y, shr64<7>(x), shr64<6>(y), P0, P1);
-		w[T & 15] += P1 + w[(T - 7) & 15] + P0;
-		return w[T & 15];
-	}
-	w[T & 15] += ssig1_512(w[(T - 2) & 15]) + w[(T - 7) & 15] +
-	    ssig0_512(w[(T - 15) & 15]);
+	const uint64_t x = w[(T - 15) & 15], y = w[(T - 2) & 15];
+	uint64_t P0, P1;
+	ssigmas512_asm(x, y, shr64<7>(x), shr64<6>(y), P0, P1);
+	w[T & 15] += P1 + w[(T - 7) & 15] + P0;
 	return w[T & 15];
 }
 
 /*
- * W[t] + K[t] for SHA-512.  NET2_KM512 selects how the 64-bit constant
- * enters the sum:
- *   0: plain C -- hipcc parks all 80 constants in SGPR pairs and spills ~100
- *      SGPRs into VGPR lanes (v_writelane/v_readlane on every block);
- *   2: a per-workgroup LDS copy of K (k512_lds, filled by
- *      k512_lds_fill() at kernel entry), read with one broadcast
- *      ds_read_b64 per round: the constant costs an LDS issue slot instead of
- *      VALU time or SGPRs.  The read is volatile so it is not hoisted out of
- *      the block loop (which would pin 160 VGPRs).  But a volatile read
- *      cannot be sunk either: when a compression's result is only used
- *      under a lane condition (a tail block, an HMAC key block, a store
- *      behind `if (live)`), the compiler sinks the rounds into that branch
- *      and leaves all 80 reads above it, live at once (HMAC-SHA512 reached
- *      400 VGPRs);
- *   3: as 2, but plain (non-volatile) reads through a base address offset
- *      by an opaque per-compression zero (an `s_mov_b32 0` the compiler
- *      cannot see through): loop-variant, so not hoisted out of the block
- *      loop, yet free to move with the rounds that consume them.
+ * W[t] + K[t] for SHA-512: a per-workgroup LDS copy of K (k512_lds, filled
+ * by k512_lds_fill() at kernel entry), read with one broadcast ds_read_b64
+ * per round, so the constant costs an LDS issue slot instead of VALU time or
+ * SGPRs (left as plain C constants, hipcc parks all 80 in SGPR pairs and
+ * spills ~100 SGPRs into VGPR lanes).  The reads are plain (non-volatile)
+ * loads through a base address offset by an opaque per-compression zero (an
+ * `s_mov_b32 0` the compiler cannot see through): loop-variant, so not
+ * hoisted out of the block loop (which would pin 160 VGPRs), yet free to
+ * move with the rounds that consume them (a volatile read cannot be sunk:
+ * when a compression's result is used only under a lane condition, the
+ * compiler sank the rounds into the branch and left all 80 reads above it,
+ * live at once -- HMAC-SHA512 reached 400 VGPRs).
  */
-#ifndef NET2_KM512
-#define NET2_KM512 3
-#endif
 typedef __attribute__((address_space(3))) uint64_t lds_k64;
 __shared__ uint64_t k512_lds[160];	/* [0,80) K512, [80,160) pad K+W */
 
@@ -649,17 +534,14 @@ __shared__ uint64_t k512_lds[160];	/* [0,80) K512, [80,160) pad K+W */
  */
 __device__ __forceinline__ void k512_lds_fill()
 {
-#if NET2_KM512 >= 2
 	for (unsigned i = threadIdx.x; i < 80; i += blockDim.x)
 		k512_lds[i] = K512[i];
 	__syncthreads();
-#endif
 }
 
 template <class PAD>
 __device__ __forceinline__ void k512_lds_fill_pad(const PAD &pad)
 {
-#if NET2_KM512 >= 2
 	for (unsigned i = threadIdx.x; i < 80; i += blockDim.x)
 		k512_lds[i] = K512[i];
 	if (threadIdx.x < 64) {
@@ -675,58 +557,26 @@ __device__ __forceinline__ void k512_lds_fill_pad(const PAD &pad)
 				k512_lds[80 + t] = pad.kw[t];
 	}
 	__syncthreads();
-#endif
 }
 
-/* Base of the LDS constant table for one compression (see NET2_KM512). */
+/* Base of the LDS constant table for one compression (the opaque zero). */
 __device__ __forceinline__ const lds_k64 *k512_base()
 {
-#if NET2_KM512 == 3
 	uint32_t z;
 	asm volatile("s_mov_b32 %0, 0" : "=s"(z));
 	return (const lds_k64 *)k512_lds + z;
-#else
-	return (const lds_k64 *)k512_lds;
-#endif
 }
 
 template <int T>
 __device__ __forceinline__ uint64_t k512_at(const lds_k64 *kb)
 {
-#if NET2_KM512 == 3
 	return kb[T];
-#elif NET2_KM512 == 2
-	typedef __attribute__((address_space(3))) volatile uint64_t lds_u64;
-	return ((const lds_u64 *)kb)[T];
-#else
-	(void)kb;
-	return T < 80 ? K512[T] : 0;
-#endif
 }
 
 template <int T>
 __device__ __forceinline__ uint64_t addk512(uint64_t w, const lds_k64 *kb)
 {
 	return w + k512_at<T>(kb);
-}
-
-/*
- * Scheduling fence every NET2_SB512 rounds.  Without it the machine
- * scheduler may hoist all 80 LDS constant reads of a straight-line
- * compression (a tail or HMAC block outside the block loop) to its top,
- * which pins 160 extra VGPRs (var/HMAC SHA-512 kernels went to 220-400
- * VGPRs, i.e. 1-2 waves per SIMD).  0 disables the fences.
- */
-#ifndef NET2_SB512
-#define NET2_SB512 0
-#endif
-template <int T>
-__device__ __forceinline__ void fence512()
-{
-#if NET2_SB512 > 0
-	if (T % NET2_SB512 == NET2_SB512 - 1)
-		__builtin_amdgcn_sched_barrier(0);
-#endif
 }
 
 template <int T>
@@ -736,7 +586,6 @@ struct Rounds512 {
 	{
 		uint64_t wt = T < 16 ? w[T & 15] : expand512<T>(w);
 		round512<T>(s, addk512<T>(wt, kb));
-		fence512<T>();
 		Rounds512<T + 1>::run(s, w, kb);
 	}
 };
@@ -765,14 +614,9 @@ struct RoundsKW512 {
 	__device__ __forceinline__ static void run(uint64_t (&s)[8],
 	    const uint64_t *kw, const lds_k64 *kb)
 	{
-#if NET2_KM512 >= 2
+		/* the pad block's K + W sit in k512_lds[80, 160) */
 		round512<T>(s, k512_at<80 + T>(kb));
 		(void)kw;
-#else
-		(void)kb;
-		round512<T>(s, kw[T]);
-#endif
-		fence512<T>();
 		RoundsKW512<T + 1>::run(s, kw, kb);
 	}
 };

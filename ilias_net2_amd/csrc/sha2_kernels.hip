@@ -29,17 +29,25 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+#include <atomic>
+
 namespace net2 {
 namespace dev {
 
 /* ---- hash traits ------------------------------------------------------ */
 
 /*
- * Per-kernel code-shape choices (each measured, DESIGN.md 5.1):
- *   ASM: round bodies as ordered asm blocks (NET2_ASM256, sha2_device.h);
+ * Per-kernel code-shape choices (each measured, DESIGN.md 5.1-5.2):
+ *   ASM: round bodies as ordered asm blocks (round256_asm, sha2_device.h);
  *   U2:  the two-block ping-pong block loop (absorb below);
  *   PAIR: the pair loop -- both 64-byte blocks of a 128-byte line requested
- *         together, one pair ahead (absorb below).
+ *         together, one pair ahead (absorb below);
+ *   DRAIN: issue priority while the grid drains (prio_remaining);
+ *   GLDS: LDS-DMA staging of the next block (absorb);
+ *   PREFETCH: block k+1 in flight while block k is compressed.
+ * Alternatives that lost their A/B (the evidence stays
+ * under profiles/) are removed from the source, not kept behind switches.
  */
 template <bool ASM_, bool U2_, bool PAIR_ = false, bool DRAIN_ = false>
 struct Sha256T {
@@ -77,85 +85,34 @@ struct Sha256T {
 			o[i] = bswap32(st[i]);
 	}
 };
-#ifndef NET2_ABSORB_U2
-#define NET2_ABSORB_U2 1
-#endif
-/* pair loop (absorb) per kernel: fixed, HMAC digests and the variable-length
- * kernel (137 VGPRs, 3 waves/SIMD, still +0.7 % on C3:
- * profiles/round1/var_pair_ab.txt); the RX verify kernel keeps the one-block
- * loop (NoPair below) */
-#ifndef NET2_FIXED_PAIR
-#define NET2_FIXED_PAIR 1
-#endif
-#ifndef NET2_HMAC_PAIR
-#define NET2_HMAC_PAIR 1
-#endif
-/* ordered asm rounds in the variable-length kernel: C3 452 against 463 us,
- * {63, 511, 1499} B 481 against 494 us (round 2, three alternations,
- * profiles/round2/var_asm_ab.txt) */
-#ifndef NET2_VAR_ASM
-#define NET2_VAR_ASM 1
-#endif
-#ifndef NET2_VAR_U2
-#define NET2_VAR_U2 1
-#endif
-/* prefetch in the byte-aligned (A1) path of the variable-length and HMAC
- * kernels: every path of a kernel shares its VGPR allocation, and the A1
- * path's double buffer (17 words each) sets it.  Variable-length kernel:
- * off since the end of round 2 -- 96 VGPRs (5 waves per SIMD) instead of
- * 105, byte-aligned mix +0.7 %, C3 +0.3 % with the A/B order flipped
- * every alternation (profiles/round2/var_a1_prefetch_ab.txt; the earlier
- * -1.6 % on C3 was measured with the variant always second) */
-#ifndef NET2_VAR_A1_PREFETCH
-#define NET2_VAR_A1_PREFETCH 0
-#endif
-#ifndef NET2_HMAC_A1_PREFETCH
-#define NET2_HMAC_A1_PREFETCH 1
-#endif
-#ifndef NET2_HMAC_ASM
-#define NET2_HMAC_ASM 1
-#endif
-#ifndef NET2_HMAC_U2
-#define NET2_HMAC_U2 1
-#endif
-typedef Sha256T<NET2_ASM256 != 0, NET2_ABSORB_U2 != 0, NET2_FIXED_PAIR != 0> Sha256;	/* fixed */
-#ifndef NET2_VAR_PAIR
-#define NET2_VAR_PAIR 1
-#endif
-/* drain priority (prio_remaining) in the variable-length kernel (A/B only,
- * off): +1.1 to +1.4 % on C3 when run second in each alternation, -0.6 %
- * when run first -- within the position effect of the A/B itself
- * (profiles/round2/var_drain_ab.txt) */
-#ifndef NET2_VAR256_DRAIN
-#define NET2_VAR256_DRAIN 0
-#endif
-typedef Sha256T<NET2_VAR_ASM != 0, NET2_VAR_U2 != 0, NET2_VAR_PAIR != 0,
-    NET2_VAR256_DRAIN != 0> Sha256V;	/* var */
-typedef Sha256T<NET2_HMAC_ASM != 0, NET2_HMAC_U2 != 0, NET2_HMAC_PAIR != 0> Sha256H;	/* HMAC */
+/*
+ * Every SHA-256 kernel takes the asm rounds, the two-block loop and the
+ * pair loop (fixed kernel: 92 VGPRs; variable-length kernel: 96, C3 +0.7 %
+ * with the pair loop, profiles/round1/var_pair_ab.txt; C3 452 against
+ * 463 us with the asm rounds, profiles/round2/var_asm_ab.txt).  The RX
+ * verify kernel drops the pair loop (NoPair below).
+ */
+typedef Sha256T<true, true, true> Sha256;	/* fixed, variable, HMAC */
+typedef Sha256 Sha256V;
+typedef Sha256 Sha256H;
 
-#ifndef NET2_FIXED512_PF
-#define NET2_FIXED512_PF 0
-#endif
-/* drain priority in the fixed SHA-512 kernel (prio_remaining below) */
-#ifndef NET2_SHA512_DRAIN
-#define NET2_SHA512_DRAIN 1
-#endif
 struct Sha512 {
 	static constexpr bool ASM = false;
-	/* no prefetch: nothing to ping-pong (NET2_FIXED512_PF=1: the two-block
-	 * ping-pong prefetch, A/B only) */
-	static constexpr bool U2 = NET2_FIXED512_PF != 0;
+	/* no prefetch: a 128-byte block would cost 32 VGPRs and a wave per
+	 * SIMD (the two-block ping-pong: -1.4 %, with 5 waves -18 %,
+	 * profiles/round2/fixed512_prefetch_ab.txt) */
+	static constexpr bool U2 = false;
 	static constexpr bool PAIR = false;	/* a 128-byte block is a whole line */
-	/* drain priority (prio_remaining): the fixed kernel only */
-	static constexpr bool DRAIN = NET2_SHA512_DRAIN != 0;
+	/* drain priority (prio_remaining): the fixed kernel only, C4 +1.2 %
+	 * (profiles/round2/drain_prio_ab.txt) */
+	static constexpr bool DRAIN = true;
 	static constexpr bool GLDS = false;
 	typedef uint64_t word;
 	static constexpr int BLOCK = 128;
 	static constexpr int NW32 = 32;
 	static constexpr int LENBYTES = 16;
 	static constexpr int DLEN = 64;		/* 48 for SHA-384 */
-	/* a 128-byte prefetch would cost 32 VGPRs and a wave per SIMD */
-	static constexpr bool PREFETCH = NET2_FIXED512_PF != 0;
+	static constexpr bool PREFETCH = false;
 	typedef uint64_t State[8];
 
 	__device__ __forceinline__ static void init(State &st, int is384)
@@ -185,52 +142,36 @@ struct Sha512 {
 };
 
 /*
- * NET2_GLDS512 (bit per kernel family: 1 variable-length SHA-512, 2 the
- * variable-length HMAC-SHA512 kernels incl. bursts, 4 the fixed-layout
- * HMAC-SHA512 kernel): the next 128-byte block is fetched with LDS-DMA
- * (global_load_lds) into a per-wave LDS slab while the current one is
- * compressed -- a prefetch that costs no VGPRs (absorb below).
+ * SHA-512 for the variable-length kernel: no prefetch -- neither the
+ * two-block ping-pong (136-140 VGPRs, 3 waves; +1.9 % on c3_512 on one box,
+ * -1.3 % on another, -3 to -4 % on the HMAC-SHA512 MTU configs and both
+ * bursts) nor LDS-DMA staging (-1.4 to -2.8 %, profiles/round3/glds_*_ab.txt).
  */
-#ifndef NET2_GLDS512
-#define NET2_GLDS512 0x4
-#endif
-/* SHA-512 for the variable-length kernel; NET2_VAR512_PF=1 (A/B only)
- * gives it the two-block ping-pong prefetch the SHA-256 kernels have. */
-#ifndef NET2_VAR512_PF
-#define NET2_VAR512_PF 0
-#endif
 struct Sha512V : Sha512 {
 	static constexpr bool DRAIN = false;
-	static constexpr bool GLDS = (NET2_GLDS512 & 1) != 0;
-	static constexpr bool U2 = NET2_VAR512_PF != 0 && !GLDS;
-	static constexpr bool PREFETCH = NET2_VAR512_PF != 0 && !GLDS;
 };
-/* ... for the lane-per-job kernel of the coalescer (NET2_JOB512_PF, on),
- * whose blocks come over PCIe from zero-copy staging: the next block's
- * load is in flight while one is compressed (64 threads of 1 KiB SHA-512
- * calls: 431 k against 399 k calls/s,
- * profiles/round2/coalesce_job512_prefetch_ab.txt) ... */
-#ifndef NET2_JOB512_PF
-#define NET2_JOB512_PF 1
-#endif
+/* ... for the lane-per-job kernel of the coalescer, whose blocks come over
+ * PCIe from zero-copy staging: the next block's load is in flight while one
+ * is compressed (64 threads of 1 KiB SHA-512 calls: 431 k against 399 k
+ * calls/s, profiles/round2/coalesce_job512_prefetch_ab.txt) ... */
 struct Sha512J : Sha512 {
 	static constexpr bool DRAIN = false;
-	static constexpr bool U2 = NET2_JOB512_PF != 0;
-	static constexpr bool PREFETCH = NET2_JOB512_PF != 0;
+	static constexpr bool U2 = true;
+	static constexpr bool PREFETCH = true;
 };
-/* ... and for the variable-length HMAC kernels (NET2_HMAC512_PF) */
-#ifndef NET2_HMAC512_PF
-#define NET2_HMAC512_PF 0
-#endif
+/* ... for the variable-length HMAC kernels (as Sha512V) ... */
 struct Sha512H : Sha512 {
 	static constexpr bool DRAIN = false;
-	static constexpr bool GLDS = (NET2_GLDS512 & 2) != 0;
-	static constexpr bool U2 = NET2_HMAC512_PF != 0 && !GLDS;
-	static constexpr bool PREFETCH = NET2_HMAC512_PF != 0 && !GLDS;
 };
-/* ... and for the fixed-layout HMAC-SHA512 kernel (drain priority kept) */
+/* ... and for the fixed-layout HMAC-SHA512 kernel: drain priority kept, the
+ * next block fetched with LDS-DMA (global_load_lds) into a per-wave LDS slab
+ * while the current one is compressed -- a prefetch that costs no VGPRs
+ * (absorb below; spill-free, profiles/round3/hmac512_spillfree_ab*.txt) */
+#ifndef NET2_HF_GLDS
+#define NET2_HF_GLDS 0
+#endif
 struct Sha512HF : Sha512 {
-	static constexpr bool GLDS = (NET2_GLDS512 & 4) != 0;
+	static constexpr bool GLDS = NET2_HF_GLDS != 0;
 };
 
 /* ---- message loading ------------------------------------------------- */
@@ -246,30 +187,21 @@ struct Sha512HF : Sha512 {
  */
 enum { AMODE_A16 = 0, AMODE_A1 = 1, AMODE_A4 = 2 };
 /*
- * NET2_ONEPATH256 / NET2_ONEPATH512: the variable-length and HMAC kernels take the A16 block
- * loads (global_load_dwordx4 at the block start) whatever the packet's
- * alignment, relying on the unaligned access mode ROCm sets for gfx9+
- * global memory (tools/unaligned_probe.hip: every byte offset reads the
- * right bytes on gfx950, profiles/round4/unaligned_probe.json): one code
- * path per kernel instead of three chosen per wave (A16 / A4 / A1).  The
- * tail block keeps its aligned-dword reads (it never touches a byte past
- * the packet).  A misaligned dwordx4 costs the memory pipeline more (a
- * pure load stream at byte offset 1: 59 against 22 us).  Per hash family,
- * from order-flipped A/Bs on separate boxes (profiles/round4/ab_*.txt): the
- * SHA-512 kernels take the one path (HMAC-SHA512 verify +2.8 %, burst RX
- * +2 %, c3_512 +0.5 to +1.2 %), the SHA-256 kernels keep the three
- * (HMAC-SHA256 verify 1.5 % and C3 0.45 % faster with them).
+ * One address path for the SHA-512 variable-length and HMAC kernels: they
+ * take the A16 block loads (global_load_dwordx4 at the block start) whatever
+ * the packet's alignment, relying on the unaligned access mode ROCm sets for
+ * gfx9+ global memory (tools/unaligned_probe.hip: every byte offset reads
+ * the right bytes on gfx950, profiles/round4/unaligned_probe.json) -- one
+ * code path per kernel instead of three chosen per wave.  The tail block
+ * keeps its aligned-dword reads (it never touches a byte past the packet).
+ * From order-flipped A/Bs on separate boxes (profiles/round4/ab_*.txt): the
+ * SHA-512 kernels gain (HMAC-SHA512 verify +2.8 %, burst RX +2 %, c3_512
+ * +0.5 to +1.2 %), the SHA-256 kernels keep the three paths (HMAC-SHA256
+ * verify 1.5 % and C3 0.45 % faster with them).
  */
-#ifndef NET2_ONEPATH256
-#define NET2_ONEPATH256 0
-#endif
-#ifndef NET2_ONEPATH512
-#define NET2_ONEPATH512 1
-#endif
 template <class H>
 struct OnePath {
-	static constexpr bool value = sizeof(typename H::word) == 8 ?
-	    NET2_ONEPATH512 != 0 : NET2_ONEPATH256 != 0;
+	static constexpr bool value = sizeof(typename H::word) == 8;
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -464,32 +396,24 @@ __device__ __forceinline__ void materialize(const typename H::State &st)
  * The SIMD's VALU arbiter serves the oldest wave first, so when the grid's
  * last generation of waves is dispatched, the youngest waves -- those with
  * the most blocks left -- progress last and finish alone, at one wave's
- * issue rate.  In the workgroups of the grid's last NET2_PRIO_GEN x 256 (two
+ * issue rate.  In the workgroups of the grid's last kPrioGen x 256 (two
  * per CU), a wave's priority follows the work it has left (s_setprio 3..0
  * as its remaining blocks fall below 12 / 6 / 2), so the waves of a SIMD
  * end closer together.  C4 +1.0 % (six alternations on two boxes; one or
  * three / four generations: +0.7 % / flat), C2 flat
- * (profiles/round2/drain_prio_ab.txt).
- *
- * NET2_PRIO (A/B only) overrides it for every kernel: 1 = the same
- * priority in every wave of the grid -- slower, C2 -5 %, C4 -6 %, C3 -1 %
- * (profiles/round2/prio_ab.txt): the age order keeps the waves of a SIMD out
- * of phase, so their loads do not all wait at once; 2 = drain-only.
+ * (profiles/round2/drain_prio_ab.txt).  The same priority in every wave of
+ * the grid measured slower (C2 -5 %, C4 -6 %, C3 -1 %,
+ * profiles/round2/prio_ab.txt): the age order keeps the waves of a SIMD out
+ * of phase, so their loads do not all wait at once.
  */
-#ifndef NET2_PRIO
-#define NET2_PRIO 0
-#endif
-#ifndef NET2_PRIO_GEN
-#define NET2_PRIO_GEN 2
-#endif
+constexpr unsigned kPrioGen = 2;
 template <bool DRAIN>
 __device__ __forceinline__ void prio_remaining(uint32_t rem_blocks)
 {
-	constexpr int mode = NET2_PRIO ? NET2_PRIO : DRAIN ? 2 : 0;
-	if (mode == 0)
+	if (!DRAIN)
 		return;
-	if (mode == 2 && (gridDim.x < 4 * 256 * NET2_PRIO_GEN ||
-	    blockIdx.x + 256 * NET2_PRIO_GEN < gridDim.x))
+	if (gridDim.x < 4 * 256 * kPrioGen ||
+	    blockIdx.x + 256 * kPrioGen < gridDim.x)
 		return;
 	const uint32_t r = __builtin_amdgcn_readfirstlane(rem_blocks);
 	if (r >= 12)
@@ -509,15 +433,6 @@ __device__ __forceinline__ void prio_remaining(uint32_t rem_blocks)
  * the launch is a multiple of the block size -- the constant padding block
  * whose K[t] + W[t] schedule the host precomputed (kw).
  */
-/*
- * NET2_PAIR_LATE=1 (A/B): the pair loop requests the next pair after the
- * first compression of the current one instead of before it, so a grid's
- * first wave generation asks HBM for one line per lane, not two, before it
- * can start.
- */
-#ifndef NET2_PAIR_LATE
-#define NET2_PAIR_LATE 0
-#endif
 /*
  * SHA*Update over the len / BLOCK full blocks at p (src/sha2.c:477-485:
  * whole blocks are transformed straight from caller memory).  With
@@ -576,17 +491,15 @@ __device__ __forceinline__ void absorb(const uint8_t *p, uint32_t len,
 		for (; q + 2 <= npairs; q += 2) {
 			prio_remaining<H::DRAIN && AMODE != AMODE_A1>(nfull - 2 * q);
 			const uint8_t *bp = p + (size_t)q * 2 * H::BLOCK;
-			if (!NET2_PAIR_LATE) {
-				issue_block<NW32, AMODE>(bp + 2 * H::BLOCK, b0);
-				issue_block<NW32, AMODE>(bp + 3 * H::BLOCK, b1);
-			}
+			/* (requested one compression later instead, so the first
+			 * wave generation asks for one line per lane before it
+			 * starts: C2 -0.3 %, HMAC-SHA256 -0.9 %,
+			 * profiles/round2/pair_late_ab.txt) */
+			issue_block<NW32, AMODE>(bp + 2 * H::BLOCK, b0);
+			issue_block<NW32, AMODE>(bp + 3 * H::BLOCK, b1);
 			uint32_t w[NW32];
 			finish_block<NW32, AMODE>(bp, a0, w);
 			H::compress(st, w);
-			if (NET2_PAIR_LATE) {
-				issue_block<NW32, AMODE>(bp + 2 * H::BLOCK, b0);
-				issue_block<NW32, AMODE>(bp + 3 * H::BLOCK, b1);
-			}
 			finish_block<NW32, AMODE>(bp + H::BLOCK, a1, w);
 			H::compress(st, w);
 			/* past the last pair: re-read pair q + 1 (in bounds, L2-hot,
@@ -748,18 +661,10 @@ __device__ __forceinline__ void fixed_lane(uint64_t i,
 		store_digest<H::DLEN>(out + i * H::DLEN, o);
 }
 
-/* waves per SIMD asked of the fixed SHA-512 kernel (A/B; 1 = no request) */
-#ifndef NET2_FIXED512_WAVES
-#define NET2_FIXED512_WAVES 1
-#endif
-template <class H>
-struct FixedWaves {
-	static constexpr int value = sizeof(typename H::word) == 8 ?
-	    NET2_FIXED512_WAVES : 1;
-};
+/* (no occupancy request: 6 waves per SIMD asked of the fixed SHA-512
+ * kernel measured -1.4 %, profiles/round2/occupancy_request_ab.txt) */
 template <class H, int AMODE, bool PADCONST>
-__global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(FixedWaves<H>::value))) void fixed_kernel(const uint8_t *__restrict__ base,
+__global__ __launch_bounds__(256) void fixed_kernel(const uint8_t *__restrict__ base,
     uint64_t stride, uint32_t len, uint64_t n, uint8_t *__restrict__ out,
     uint32_t dlen, int is384, PadKW<typename H::word> pad)
 {
@@ -786,9 +691,6 @@ __attribute__((amdgpu_waves_per_eu(FixedWaves<H>::value))) void fixed_kernel(con
  * expanding it (48 of 64 schedule words, ~480 VALU instructions per lane),
  * as fixed_kernel does with its kernel-argument copy.
  */
-#ifndef NET2_PADTAB
-#define NET2_PADTAB 1
-#endif
 #define NET2_PADTAB_N 1026
 
 struct PadTab256 {
@@ -833,7 +735,7 @@ template <class H>
 __device__ __forceinline__ const typename H::word *uniform_pad_kw(bool live,
     uint64_t bytes)
 {
-	if (!NET2_PADTAB || sizeof(typename H::word) != 4)
+	if (sizeof(typename H::word) != 4)
 		return nullptr;
 	const uint32_t lo = (uint32_t)bytes;
 	const uint32_t b0 = __builtin_amdgcn_readfirstlane(lo);
@@ -849,7 +751,7 @@ __device__ __forceinline__ const typename H::word *uniform_pad_kw(bool live,
  * message (0x80, zeros, 128-bit bit count 1024 * j; SHA512Pad,
  * src/sha2.c:784-832) for j < NET2_PADTAB512_N, 329 KB of constant memory.
  * SHA-512 compressions read their round constants from the workgroup's LDS
- * copy (k512_lds, NET2_KM512), so the table row is staged there, in the
+ * copy (k512_lds, sha2_device.h), so the table row is staged there, in the
  * [80, 160) half the fixed kernel's constant pad block uses; that makes the
  * choice per workgroup: every live lane of it must share the length.
  */
@@ -893,8 +795,6 @@ __constant__ const PadTab512 g_padtab512 = make_padtab512();
  */
 __device__ __forceinline__ bool block_pad512(bool live, uint64_t bytes)
 {
-	if (!NET2_PADTAB)
-		return false;
 	__shared__ uint64_t b0s;
 	if (threadIdx.x == 0)
 		b0s = live ? bytes : 1;	/* thread 0 is live if any thread is */
@@ -963,26 +863,31 @@ __device__ __forceinline__ void var_digest(const uint8_t *p, uint32_t len,
 }
 
 /*
+ * The visiting order a launch's binning left in ws (sha2_launch.h): perm,
+ * or submission order (nullptr) when ws is NULL or when that binning launch
+ * -- the one tagged `launch` -- found its global histogram inconsistent
+ * (BinHdr::bad == launch, bin_onepass_kernel): its workgroups may then have
+ * written a mix of binned and identity positions.  One scalar load.
+ */
+__device__ __forceinline__ const uint32_t *bin_perm(
+    const uint32_t *__restrict__ ws, uint32_t launch)
+{
+	if (ws == nullptr || ws[NET2_BIN_W_BAD] == launch)
+		return nullptr;
+	return ws + NET2_BIN_WS_WORDS;
+}
+
+/*
  * Variable-length packets, visited in binned order: lane g hashes packet
  * perm[g] (perm == NULL: identity).  The address mode is chosen per wave:
  * if every lane's packet start is 16-byte aligned the wave takes the vector
  * load path, else the byte-aligned one.  A SHA-256 wave (SHA-512:
  * workgroup) of one whole-block length, e.g. a bin of a batch of fixed
  * sizes, takes its pad schedule from g_padtab256 (g_padtab512).
+ * (No occupancy request: 5 waves asked of the variable-length SHA-256
+ * kernel measured flat, of the SHA-512 one -2 %,
+ * profiles/round2/occupancy_request_ab.txt.)
  */
-/* waves per SIMD asked of the variable-length kernel, per word size
- * (A/B; 1 = no request: the VGPR count decides) */
-#ifndef NET2_VAR256_WAVES
-#define NET2_VAR256_WAVES 1
-#endif
-#ifndef NET2_VAR512_WAVES
-#define NET2_VAR512_WAVES 1
-#endif
-template <class H>
-struct VarWaves {
-	static constexpr int value = sizeof(typename H::word) == 8 ?
-	    NET2_VAR512_WAVES : NET2_VAR256_WAVES;
-};
 /* One packet of var_kernel: binned position g (SHA-512: block_pad512 is a
  * workgroup barrier, so every thread calls this equally often). */
 template <class H>
@@ -1009,9 +914,11 @@ __device__ __forceinline__ void var_item(uint64_t g,
 	else if (__all((reinterpret_cast<uintptr_t>(p) & 3) == 0))
 		var_digest<H, AMODE_A4>(p, len, is384, kw, padtab, st);
 	else
-		var_digest<H, AMODE_A1,
-		    H::PREFETCH && NET2_VAR_A1_PREFETCH != 0>(p, len, is384, kw,
-		    padtab, st);
+		/* no prefetch on the byte-aligned path: its double buffer
+		 * (17 words each) set the kernel's VGPRs (105 against 96, 5
+		 * waves); C3 +0.3 %, byte-aligned mix +0.7 % without,
+		 * profiles/round2/var_a1_prefetch_ab.txt */
+		var_digest<H, AMODE_A1, false>(p, len, is384, kw, padtab, st);
 	materialize<H>(st);
 	if (!live)
 		return;
@@ -1023,17 +930,17 @@ __device__ __forceinline__ void var_item(uint64_t g,
 		store_digest<H::DLEN>(out + i * H::DLEN, o);
 }
 
+/* ws: the binning workspace of this launch (NULL: submission order). */
 template <class H>
-__global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(VarWaves<H>::value))) void var_kernel(const uint8_t *__restrict__ base,
+__global__ __launch_bounds__(256) void var_kernel(const uint8_t *__restrict__ base,
     const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
-    const uint32_t *__restrict__ perm, uint64_t n, uint8_t *__restrict__ out,
-    uint32_t dlen, int is384)
+    const uint32_t *__restrict__ ws, uint32_t launch, uint64_t n,
+    uint8_t *__restrict__ out, uint32_t dlen, int is384)
 {
 	if (sizeof(typename H::word) == 8)
 		k512_lds_fill();
 	var_item<H>((uint64_t)blockIdx.x * blockDim.x + threadIdx.x, base,
-	    offsets, lens, perm, n, out, dlen, is384);
+	    offsets, lens, bin_perm(ws, launch), n, out, dlen, is384);
 }
 
 /* ---- HMAC (RFC 2104) ------------------------------------------------------ */
@@ -1044,14 +951,20 @@ __attribute__((amdgpu_waves_per_eu(VarWaves<H>::value))) void var_kernel(const u
  * authenticator of net2_packet_encode/decode (types/packet.n2t:246,417),
  * over a whole batch under one connection key:
  *   HMAC(K, m) = H((K' ^ opad) || H((K' ^ ipad) || m)),  K' = K zero-padded.
- * The two key blocks are compressed once per workgroup (wave 0, wave-
- * uniform) into LDS midstates; every lane then hashes its packet from the
- * inner midstate (bit count includes the key block) and finishes with one
- * outer compression over the inner digest.
+ * The two key blocks -- the same for every packet of a launch -- are
+ * compressed once on the host (hmac_midstates below) and arrive as kernel
+ * arguments: the ipad / opad midstates, copied to LDS at kernel entry; every
+ * lane hashes its packet from the inner midstate (bit count includes the key
+ * block) and finishes with one outer compression over the inner digest.
+ * (Until round 4 wave 0 of every workgroup compressed the key blocks while
+ * the other waves waited: a second instance of the round code in the kernel,
+ * which held the fixed-layout HMAC-SHA512 kernel at 115 VGPRs.)
  */
-template <int NW32>
-struct HKey {
-	uint32_t w[NW32];	/* K' as big-endian words */
+struct HMid {
+	/* [0] K' ^ ipad, [1] K' ^ opad as digest words (SHA-256: 8 state words;
+	 * SHA-384/512: hi, lo of each 64-bit word); [2..3] the same for the
+	 * alternate rx key (HMAC_BURST_RX with rx.alt) */
+	uint32_t w[4][16];
 };
 
 /* Inner hash from the ipad midstate, one address mode. */
@@ -1082,9 +995,7 @@ __device__ __forceinline__ void hmac_lane(const uint8_t *p, uint32_t len,
 	else if (amode == AMODE_A4)
 		hmac_inner<H, AMODE_A4, PADCONST>(p, len, mid, kw, st, padtab);
 	else
-		hmac_inner<H, AMODE_A1, PADCONST,
-		    H::PREFETCH && NET2_HMAC_A1_PREFETCH != 0>(p, len, mid, kw, st,
-		    padtab);
+		hmac_inner<H, AMODE_A1, PADCONST>(p, len, mid, kw, st, padtab);
 
 	/* outer: one block = inner digest || 0x80 || 0... || bit count */
 	uint32_t w[NW32];
@@ -1163,49 +1074,28 @@ __device__ __forceinline__ uint32_t load_be32_bytes(const uint8_t *p)
  */
 /* (struct BurstArgs: sha2_launch.h) */
 
-/* VERIFY: compare the hash field in whole words when the wave's message
- * starts (and so its hash fields) are 4- or 16-byte aligned */
-#ifndef NET2_VERIFY_WORDS
-#define NET2_VERIFY_WORDS 1
-#endif
 
 
-/*
- * Occupancy of the SHA-512 HMAC kernels: NET2_HMAC512_W5 has bit MODE set
- * for the modes compiled for 5 waves per SIMD (96 VGPRs, some scratch
- * spills) instead of the 4 their 114-118 VGPRs give.  Digests: HMAC-SHA512
- * 1 KiB +4.2 %, the MTU mix +2.2 %; the RX burst mode -14.6 % (it spills
- * three times as much) (profiles/round2/hmac512_waves_ab.txt).
- */
-#ifndef NET2_HMAC512_W5
-#define NET2_HMAC512_W5 0x0
-#endif
-/* the same for the SHA-256 HMAC kernels (A/B; 0 = none) */
-#ifndef NET2_HMAC256_W5
-#define NET2_HMAC256_W5 0x0
-#endif
-template <class H, int MODE>
-struct HmacWaves {
-	/* an LDS-DMA kernel's slabs (~35 KB per workgroup) hold it at 4 waves
-	 * per SIMD whatever its VGPRs: no request */
-	static constexpr int value = !H::GLDS && ((sizeof(typename H::word) == 8 ?
-	    NET2_HMAC512_W5 : NET2_HMAC256_W5) >> MODE & 1) ? 5 : 1;
-};
 /*
  * One datagram / packet of hmac_kernel: binned position g (live: g < n).
  * Shares the workgroup's key midstates (mid) and, for SHA-512, its LDS
  * constant table; calls block_pad512 (a workgroup barrier), so every
- * thread of the workgroup calls it the same number of times.
+ * thread of the workgroup calls it the same number of times.  IS384 and
+ * the digest length are compile-time constants of the kernel instance
+ * (SHA-384 is its own instance: the outer block's 0x80 word and zero fill
+ * fold into its schedule).
  */
-template <class H, bool PADCONST, int MODE>
+template <class H, bool PADCONST, int MODE, bool IS384>
 __device__ __forceinline__ void hmac_item(uint64_t g,
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lens, const uint32_t *__restrict__ perm,
     uint64_t stride, uint32_t fixed_len, uint64_t n,
-    uint8_t *__restrict__ out, uint32_t dlen, int is384,
-    const PadKW<typename H::word> &pad, const BurstArgs &rx,
-    const uint32_t (*mid)[16])
+    uint8_t *__restrict__ out, const PadKW<typename H::word> &pad,
+    const BurstArgs &rx, const uint32_t (*mid)[16])
 {
+	constexpr int is384 = IS384;
+	constexpr uint32_t dlen = sizeof(typename H::word) == 4 ? 32 :
+	    IS384 ? 48 : 64;
 	const uint32_t (*lmid)[16] = mid;	/* this lane's key */
 	const bool live = g < n;
 	uint64_t i = g;
@@ -1222,6 +1112,9 @@ __device__ __forceinline__ void hmac_item(uint64_t g,
 		len = live ? fixed_len : 0;
 	}
 	uint32_t rx_st = PKT_OK, rx_seq = 0, rx_fl = 0;
+	/* TX with rx.rec: header and hash field to a record of their own
+	 * (field at +0, header at +dlen; the host path) instead of in place;
+	 * its address is formed where it is used (not held across the hash) */
 	if (MODE == HMAC_BURST_TX) {
 		if (live) {
 			rx_seq = rx.seq[i];
@@ -1234,11 +1127,17 @@ __device__ __forceinline__ void hmac_item(uint64_t g,
 		else if (len < 8 + dlen)
 			rx_st = PKT_RESOURCE;	/* no room for header and hash */
 		if (live && rx_st == PKT_OK) {
-			uint8_t *h = out + (p - base);
+			if (rx.rec != nullptr) {
+				*reinterpret_cast<uint2 *>(rx.rec + i * (dlen + 16) +
+				    dlen) = make_uint2(bswap32(rx_seq),
+				    bswap32(rx_fl));
+			} else {
+				uint8_t *h = out + (p - base);
 #pragma unroll
-			for (int b = 0; b < 4; b++) {
-				h[b] = (uint8_t)(rx_seq >> (24 - 8 * b));
-				h[4 + b] = (uint8_t)(rx_fl >> (24 - 8 * b));
+				for (int b = 0; b < 4; b++) {
+					h[b] = (uint8_t)(rx_seq >> (24 - 8 * b));
+					h[4 + b] = (uint8_t)(rx_fl >> (24 - 8 * b));
+				}
 			}
 			p += 8;
 			len -= 8;
@@ -1273,8 +1172,13 @@ __device__ __forceinline__ void hmac_item(uint64_t g,
 		} else {
 			len = 0;
 		}
+		/* stored now, so none of them is held across the hash */
+		if (live) {
+			rx.status[i] = (uint8_t)rx_st;
+			rx.seq[i] = rx_seq;
+			rx.flags[i] = rx_fl;
+		}
 	}
-	const uint8_t *field = p;	/* SIGN / VERIFY: the hash field */
 	const bool short_dgram = MODE != HMAC_DIGESTS && len < dlen;
 	if (MODE != HMAC_DIGESTS) {
 		p += short_dgram ? 0 : dlen;
@@ -1284,20 +1188,21 @@ __device__ __forceinline__ void hmac_item(uint64_t g,
 	const uintptr_t pa = reinterpret_cast<uintptr_t>(p);
 	const int amode = OnePath<H>::value || __all((pa & 15) == 0) ? AMODE_A16 :
 	    __all((pa & 3) == 0) ? AMODE_A4 : AMODE_A1;
-	/* a variable-layout wave (SHA-256) or workgroup (SHA-512) of one
-	 * whole-block inner length (key block included) takes its inner pad
-	 * schedule from g_padtab256 / g_padtab512 */
+	/* a variable-layout SHA-256 wave of one whole-block inner length (key
+	 * block included) takes its inner pad schedule from g_padtab256 */
 	const typename H::word *kw = nullptr;
 	bool padtab = false;
 	if constexpr (!PADCONST && sizeof(typename H::word) == 4) {
 		if (offsets != nullptr)
 			kw = uniform_pad_kw<H>(live, (uint64_t)len + H::BLOCK);
 		padtab = kw != nullptr;
-	} else if constexpr (!PADCONST) {
-		/* SHA-512: per workgroup, staged in k512_lds (block_pad512) */
-		if (offsets != nullptr)
-			padtab = block_pad512(live, (uint64_t)len + H::BLOCK);
 	}
+	/* (SHA-512: no pad table.  The workgroup-uniform g_padtab512 row the
+	 * variable-length digest kernel stages costs these kernels 11 VGPRs --
+	 * 106-107 against 95-96, four waves per SIMD instead of five -- and
+	 * pays only when a whole workgroup's inner lengths are one multiple of
+	 * 128 bytes, which no MTU mix has: payload + 128-byte key block of
+	 * {64, 512, 1428 / 1500} B.) */
 	hmac_lane<H, PADCONST>(p, len, is384, amode, lmid,
 	    kw != nullptr ? kw : pad.kw, st, padtab);
 	materialize<H>(st);
@@ -1305,100 +1210,95 @@ __device__ __forceinline__ void hmac_item(uint64_t g,
 		return;
 	uint32_t o[16];
 	H::out_words(st, o, is384);
+	/* SIGN / VERIFY: the hash field, found again from the descriptor (one
+	 * L2-hot load) rather than held in two VGPRs across the hash: the
+	 * datagram's start, past the header in the burst modes */
+	const uint8_t *field = MODE == HMAC_DIGESTS ? nullptr :
+	    base + offsets[i] + (MODE == HMAC_BURST_RX || MODE == HMAC_BURST_TX ?
+	    8 : 0);
 	if (MODE == HMAC_VERIFY || MODE == HMAC_BURST_RX) {
 		/* o[] holds the digest bytes little-endian per word, the order
 		 * store_digest writes them in */
 		uint32_t diff = 0;
-		constexpr int NO = H::DLEN / 4;	/* dlen / 4 <= NO (SHA-384: 12) */
-		if (!short_dgram && NET2_VERIFY_WORDS && amode == AMODE_A16) {
-			/* field = message start - dlen: 16-byte aligned as well;
+		constexpr int NO = dlen / 4;
+		if (!short_dgram && amode == AMODE_A16) {
+			/* field = message start - dlen: 16-byte aligned as well
+			 * (SHA-512: the one address path reads it at any alignment);
 			 * all loads issued at once (a per-byte loop waited out one
 			 * memory latency per byte) */
 			const u32x4 *f = reinterpret_cast<const u32x4 *>(field);
 #pragma unroll
-			for (int k = 0; k < NO / 4; k++)
-				if (16 * k < (int)dlen) {
-					const u32x4 v = f[k];
-					diff |= (v.x ^ o[4 * k]) | (v.y ^ o[4 * k + 1]) |
-					    (v.z ^ o[4 * k + 2]) | (v.w ^ o[4 * k + 3]);
-				}
-		} else if (!short_dgram && NET2_VERIFY_WORDS &&
-		    amode == AMODE_A4) {
+			for (int k = 0; k < NO / 4; k++) {
+				const u32x4 v = f[k];
+				diff |= (v.x ^ o[4 * k]) | (v.y ^ o[4 * k + 1]) |
+				    (v.z ^ o[4 * k + 2]) | (v.w ^ o[4 * k + 3]);
+			}
+		} else if (!short_dgram && amode == AMODE_A4) {
 			const uint32_t *f = reinterpret_cast<const uint32_t *>(field);
 #pragma unroll
 			for (int k = 0; k < NO; k++)
-				if (4 * k < (int)dlen)
-					diff |= f[k] ^ o[k];
+				diff |= f[k] ^ o[k];
 		} else if (!short_dgram) {
 #pragma unroll
-			for (int j = 0; j < 4 * NO; j++)
-				if (j < (int)dlen)
-					diff |= field[j] ^
-					    ((o[j >> 2] >> (8 * (j & 3))) & 0xffu);
+			for (int j = 0; j < (int)dlen; j++)
+				diff |= field[j] ^
+				    ((o[j >> 2] >> (8 * (j & 3))) & 0xffu);
 		}
 		out[i] = short_dgram ? 2 : diff != 0;
-		if (MODE == HMAC_BURST_RX) {
-			rx.status[i] = (uint8_t)rx_st;
-			rx.seq[i] = rx_seq;
-			rx.flags[i] = rx_fl;
-		}
 		return;
 	}
 	constexpr bool SIGNS = MODE == HMAC_SIGN || MODE == HMAC_BURST_TX;
-	uint8_t *dst = SIGNS ? out + (field - base) : out + i * dlen;
 	if (SIGNS && short_dgram)
 		return;
-	if (dlen == 48)
-		store_digest<48>(dst, o);
-	else if (dlen == 32)
-		store_digest<32>(dst, o);
+	if (MODE == HMAC_BURST_TX && rx.rec != nullptr)
+		store_digest<dlen>(rx.rec + i * (dlen + 16), o);
 	else
-		store_digest<64>(dst, o);
+		store_digest<dlen>(SIGNS ? out + (field - base) : out + i * dlen,
+		    o);
 }
 
-template <class H, bool PADCONST, int MODE = HMAC_DIGESTS>
-__global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(HmacWaves<H, MODE>::value))) void hmac_kernel(const uint8_t *__restrict__ base,
+/*
+ * ws: the binning workspace of this launch (variable layout; NULL:
+ * submission order); hm: the key's midstates (HMid).  No occupancy request:
+ * 5 waves asked of the SHA-512 kernels measured +3-4 % on the digests only
+ * while they spilled, and -2 to -15 % on the sign / verify / burst modes
+ * (round 2, profiles/round2/hmac512_waves_ab.txt); the VGPR count decides.
+ */
+template <class H, bool PADCONST, int MODE, bool IS384>
+__global__ __launch_bounds__(256) void hmac_kernel(const uint8_t *__restrict__ base,
     const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
-    const uint32_t *__restrict__ perm, uint64_t stride, uint32_t fixed_len,
-    uint64_t n, uint8_t *__restrict__ out, uint32_t dlen, int is384,
-    HKey<H::NW32> key, PadKW<typename H::word> pad, BurstArgs rx)
+    const uint32_t *__restrict__ ws, uint32_t launch, uint64_t stride,
+    uint32_t fixed_len, uint64_t n, uint8_t *__restrict__ out, HMid hm,
+    PadKW<typename H::word> pad, BurstArgs rx)
 {
-	constexpr int NW32 = H::NW32;
 	/* [0..1]: the key's ipad / opad midstates; [2..3]: the alternate rx
 	 * key's (HMAC_BURST_RX with rx.alt) */
 	__shared__ uint32_t mid[4][16];
 	const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	/* one lane copies them (the by-value argument read with constant
+	 * indices only: a dynamic index would copy it to scratch) */
+	if (threadIdx.x == 0) {
+		constexpr int NK = MODE == HMAC_BURST_RX ? 4 : 2;
+		/* whole chaining values (SHA-384's too) */
+		constexpr int NWD = sizeof(typename H::word) == 4 ? 8 : 16;
+#pragma unroll
+		for (int k = 0; k < NK; k++)
+#pragma unroll
+			for (int j = 0; j < NWD; j++)
+				mid[k][j] = hm.w[k][j];
+	}
 	if (sizeof(typename H::word) == 8) {
+		/* (both synchronise the workgroup) */
 		if (PADCONST)
 			k512_lds_fill_pad(pad);
 		else
 			k512_lds_fill();
+	} else {
+		__syncthreads();
 	}
-	if (threadIdx.x < 64) {
-		/* lane 0: K' ^ ipad, lane 1: K' ^ opad, lanes 2 / 3 the same for
-		 * the alternate key -- one compression */
-		const int pass = threadIdx.x & 1;
-		const bool alt = MODE == HMAC_BURST_RX && (threadIdx.x & 2) != 0;
-		const uint32_t pad = pass ? 0x5c5c5c5cu : 0x36363636u;
-		typename H::State ks;
-		H::init(ks, is384);
-		uint32_t w[NW32];
-#pragma unroll
-		for (int i = 0; i < NW32; i++)
-			w[i] = (alt ? rx.altkey[i] : key.w[i]) ^ pad;
-		H::compress(ks, w);
-		materialize<H>(ks);
-		uint32_t kw[NW32];
-		digest_words<H>(ks, 0, kw);
-		if (threadIdx.x < (MODE == HMAC_BURST_RX && rx.alt ? 4u : 2u))
-#pragma unroll
-			for (int i = 0; i < 16; i++)
-				mid[threadIdx.x][i] = i < (sizeof(typename H::word) == 4 ? 8 : 16) ? kw[i] : 0u;
-	}
-	__syncthreads();
-	hmac_item<H, PADCONST, MODE>(g, base, offsets, lens, perm, stride,
-	    fixed_len, n, out, dlen, is384, pad, rx, mid);
+	hmac_item<H, PADCONST, MODE, IS384>(g, base, offsets, lens,
+	    offsets != nullptr ? bin_perm(ws, launch) : nullptr, stride,
+	    fixed_len, n, out, pad, rx, mid);
 }
 
 /* ---- coalesced small jobs (sha2_coalesce.cpp) ------------------------------- */
@@ -1798,11 +1698,16 @@ __global__ __launch_bounds__(256) void burst_prep_kernel(uint8_t *__restrict__ b
 __global__ __launch_bounds__(256) void burst_final_kernel(uint64_t n,
     const uint8_t *__restrict__ status, const uint8_t *__restrict__ verdict,
     const uint32_t *__restrict__ seq, const uint32_t *__restrict__ flags,
-    uint32_t ivlen, uint8_t *__restrict__ iv, uint8_t *__restrict__ result)
+    uint32_t ivlen, uint8_t *__restrict__ iv, uint8_t *__restrict__ result,
+    uint32_t *__restrict__ seq_out, uint32_t *__restrict__ flags_out)
 {
 	const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n)
 		return;
+	if (seq_out != nullptr) {	/* the decoded header, to the host */
+		seq_out[i] = seq[i];
+		flags_out[i] = flags[i];
+	}
 	uint32_t st = status[i];
 	if (st & BURST_VERIFY)		/* net2_buffer_cmp, :253-257 */
 		st = verdict[i] == 0 ? PKT_OK : PKT_BAD;
@@ -1830,18 +1735,16 @@ __device__ __forceinline__ uint32_t bin_of(uint32_t len, int blk_shift,
  * with one tile each).  Every workgroup pays a fixed cost (clearing the
  * 2,048-bin LDS histogram, the histogram scan, its global atomics), so
  * fewer, larger tiles win down to 4,096 packets; 2,048 and 8,192 measured
- * slower (profiles/round1/binning_time_ab.txt, on the three-launch binning
- * of rounds 1-3). */
-#ifndef NET2_BIN_ITEMS
-#define NET2_BIN_ITEMS 16
-#endif
-#define NET2_BIN_TILE (256 * NET2_BIN_ITEMS)
-/* A thread's NET2_BIN_ITEMS lengths, all loads issued before any is used. */
+ * slower (profiles/round1/binning_time_ab.txt, three-launch binning;
+ * profiles/round4/bin_probe_items32_tiles8192.txt, this kernel). */
+constexpr int kBinItems = 16;
+#define NET2_BIN_TILE (256 * kBinItems)
+/* A thread's kBinItems lengths, all loads issued before any is used. */
 __device__ __forceinline__ void load_lens(const uint32_t *__restrict__ lens,
-    uint64_t n, uint64_t i0, uint32_t (&len)[NET2_BIN_ITEMS])
+    uint64_t n, uint64_t i0, uint32_t (&len)[kBinItems])
 {
 #pragma unroll
-	for (int k = 0; k < NET2_BIN_ITEMS; k++) {
+	for (int k = 0; k < kBinItems; k++) {
 		const uint64_t i = i0 + (uint64_t)k * 256;
 		len[k] = i < n ? lens[i] : 0u;
 	}
@@ -1849,8 +1752,10 @@ __device__ __forceinline__ void load_lens(const uint32_t *__restrict__ lens,
 
 /*
  * Binning in one launch (round 4; until round 3 a memset, a count and a
- * scatter launch): the count, the global prefix and the scatter, no memset.  A persistent grid of G <= 256
- * workgroups (each loops over its 4,096-packet tiles):
+ * scatter launch): the count, the global prefix and the scatter, no memset.
+ * A persistent grid of G workgroups -- at most 256, and no more than the
+ * device holds at once (the host caps G at the co-resident capacity of this
+ * kernel, net2_bin_order) -- each looping over its 4,096-packet tiles:
  *   1. LDS histogram of its tiles, each packet's rank in its bin kept in
  *      registers (the LDS atomic's return value), then one device-scope
  *      fetch-add per touched bin into the global histogram, whose old value
@@ -1861,25 +1766,38 @@ __device__ __forceinline__ void load_lens(const uint32_t *__restrict__ lens,
  *      everyone polls `state`;
  *   3. every workgroup scans the global histogram (8 KiB) for the bin
  *      bases and writes perm[base + start + rank] -- no claim pass, no
- *      second read of the lengths (a workgroup with several tiles, above
- *      256 x 4,096 packets, ranks them again from the same starts).
+ *      second read of the lengths (a workgroup with several tiles ranks
+ *      them again from the same starts).
  * The workspace cleans up after itself: the histogram and the barrier words
  * come in two parities (the epoch selects); each launch zeroes the parity
  * the next launch uses, so nothing waits for the last workgroup to leave.
  *
- * Never a hang, never a wrong order:
- *   - a barrier that does not complete within NET2_BIN_TIMEOUT (the grid
- *     not co-resident, e.g. beside many concurrent launches) is decided
+ * Never a hang, never a wrong order, and every fallback counted in the
+ * header (net2_sha2_workspace_stats):
+ *   - a barrier that does not complete within the timeout (the grid not
+ *     co-resident, e.g. beside long kernels on other streams) is decided
  *     ABORT by one compare-and-swap on `state`, which every workgroup then
  *     follows: all write the identity order (perm[i] = i, hashing in
- *     submission order: correct, only slower), and the header is marked for
- *     re-initialisation;
- *   - a workspace whose header is not initialised (the first use of a
- *     caller's buffer unless net2_sha2_workspace_init ran, or after an
- *     ABORT) takes the same identity order while workgroup 0 initialises
- *     the header and both parities, so the next launch bins;
+ *     submission order: correct, only slower), the header is marked for
+ *     re-initialisation and NET2_BIN_W_ABORTS counts it;
+ *   - a header is valid when its tag holds the magic and the id of a launch
+ *     other than this one; otherwise (fresh memory, after an ABORT or a
+ *     mismatch -- which leave a re-init mark, so the counters survive -- or
+ *     prepared by workgroup 0 of this very launch -- a workgroup dispatched
+ *     after workgroup 0 re-tagged it must not join a barrier the early ones
+ *     skipped) every workgroup takes the identity order while workgroup 0
+ *     initialises the header and both parities, so the next launch bins
+ *     (NET2_BIN_W_UNPREP counts it);
+ *   - after the barrier every workgroup checks that the global histogram
+ *     adds up to n (64-bit sum): anything else -- stale counts, or barrier
+ *     words someone else overwrote (a caller reusing the workspace for other
+ *     data) -- marks the launch bad (NET2_BIN_W_BAD = its id,
+ *     NET2_BIN_W_MISMATCH counts it) and clears the magic.  Workgroups that
+ *     read the histogram at different times may then have written a mix of
+ *     orders, so the hash kernel of this launch, given the same id, hashes
+ *     in submission order instead (bin_perm);
  *   - the hash kernels clamp perm entries to [0, n) (a corrupt workspace
- *     can cost digests, never an out-of-bounds access).
+ *     can cost the binning, never an out-of-bounds access).
  * The workspace must not be used by two launches at once (as before).
  *
  * Memory ordering.  What crosses the barrier is the histogram, written and
@@ -1892,16 +1810,15 @@ __device__ __forceinline__ void load_lens(const uint32_t *__restrict__ lens,
  * per poll ~3x (profiles/round4/bin_probe_*.txt).
  */
 #define BIN_ORD __ATOMIC_RELAXED
-#ifndef NET2_BIN_SPIN_SLEEP
-#define NET2_BIN_SPIN_SLEEP 2
-#endif
+constexpr int kBinSpinSleep = 2;
 #define NET2_BIN_GROUPS 16
 /*
  * Barrier words, per parity, in the workspace after the two histograms
  * (each word on its own 128-byte line): group counters at 32 g, the top counter
  * at 512, the state at 544.  Words 2,048-4,095 of the area hold the probe
  * stamps (NET2_BIN_PROBE=1, tools/bin_probe.py: thread 0 of every
- * workgroup stamps the 100 MHz clock at eight points).
+ * workgroup stamps the 100 MHz clock at seven points; a measurement build,
+ * never the shipped one).
  */
 #define BIN_CTL_PAR 1024
 #define BIN_CTL_TOP 512
@@ -1911,23 +1828,24 @@ __device__ __forceinline__ void load_lens(const uint32_t *__restrict__ lens,
 #endif
 #define BIN_STAMP(p) do { if (NET2_BIN_PROBE && threadIdx.x == 0) \
 	ctl0[2048 + blockIdx.x * 8 + (p)] = (uint32_t)wall_clock64(); } while (0)
-#define NET2_BIN_MAGIC 0x4e45543242494e53ull	/* "NET2BINS" */
+#define NET2_BIN_MAGIC32 0x4e324253u	/* "N2BS" */
+/* the tag after an ABORT or a mismatch: re-initialise, counters kept */
+#define NET2_BIN_REINIT32 0x4e325249u	/* "N2RI" */
 #define NET2_BIN_GRID 256
 /* 50 ms of the 100 MHz s_memrealtime clock */
 #define NET2_BIN_TIMEOUT 5000000ull
+/* the first bin of packets that need at most two compressions */
+#define NET2_BIN_SHORT (NET2_SHA2_NBINS - 3)
 
-struct BinHdr {
-	uint64_t magic;
-	uint32_t epoch;
-	uint32_t pad[NET2_BIN_HDR - 3];
-};
-static_assert(sizeof(BinHdr) == 4 * NET2_BIN_HDR, "header size");
 static_assert(NET2_BIN_CTL + 2048 + NET2_BIN_GRID * 8 <= NET2_BIN_WS_WORDS,
     "probe words");
 static_assert(NET2_BIN_HDR + 2 * NET2_SHA2_NBINS <= NET2_BIN_CTL,
     "histograms");
+static_assert(NET2_BIN_W_BINNED < NET2_BIN_HDR, "header words");
 static_assert(BIN_CTL_STATE < BIN_CTL_PAR && 32 * NET2_BIN_GROUPS <= BIN_CTL_TOP,
     "barrier words");
+static_assert(NET2_BIN_SHORT / (NET2_SHA2_NBINS / 256) == 255,
+    "the short tail's first bin is the last thread's");
 enum { BIN_UNDECIDED = 0, BIN_GO = 1, BIN_ABORT = 2 };
 
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t *p)
@@ -1935,12 +1853,23 @@ __device__ __forceinline__ uint32_t ld_agent(const uint32_t *p)
 	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+__device__ __forceinline__ void add_agent(uint32_t *p, uint32_t v)
+{
+	(void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED,
+	    __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint64_t *bin_tag(uint32_t *ws)
+{
+	return reinterpret_cast<uint64_t *>(ws + NET2_BIN_W_TAG);
+}
+
 /* perm[i] = i for this workgroup's tiles */
 __device__ __forceinline__ void bin_identity(uint32_t *perm, uint64_t n,
     uint64_t ntiles)
 {
 	for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x)
-		for (int k = 0; k < NET2_BIN_ITEMS; k++) {
+		for (int k = 0; k < kBinItems; k++) {
 			const uint64_t i = t * NET2_BIN_TILE + (uint64_t)k * 256 +
 			    threadIdx.x;
 			if (i < n)
@@ -1950,13 +1879,14 @@ __device__ __forceinline__ void bin_identity(uint32_t *perm, uint64_t n,
 
 __global__ __launch_bounds__(256) void bin_onepass_kernel(
     const uint32_t *__restrict__ lens, uint64_t n, int blk_shift,
-    int lenbytes, uint32_t *__restrict__ ws, uint64_t timeout)
+    int lenbytes, uint32_t *__restrict__ ws, uint64_t timeout,
+    uint32_t launch)
 {
 	__shared__ uint32_t cnt[NET2_SHA2_NBINS];
 	__shared__ uint32_t start[NET2_SHA2_NBINS];
 	__shared__ uint32_t wsum[4];
+	__shared__ uint64_t wtot[4];
 	__shared__ uint32_t bc[2];
-	BinHdr *h = reinterpret_cast<BinHdr *>(ws);
 	uint32_t *hist0 = ws + NET2_BIN_HDR;		/* [2][NBINS] */
 	uint32_t *ctl0 = ws + NET2_BIN_CTL;		/* [2][1024] */
 	uint32_t *perm = ws + NET2_BIN_WS_WORDS;
@@ -1965,13 +1895,15 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 	constexpr uint32_t HW = NET2_SHA2_NBINS;
 
 	/* the first tile's lengths in flight while the header is read */
-	uint32_t len[NET2_BIN_ITEMS];
+	uint32_t len[kBinItems];
 	load_lens(lens, n, (uint64_t)blockIdx.x * NET2_BIN_TILE + threadIdx.x,
 	    len);
 	if (threadIdx.x == 0) {
-		bc[0] = __hip_atomic_load(&h->magic, __ATOMIC_RELAXED,
-		    __HIP_MEMORY_SCOPE_AGENT) == NET2_BIN_MAGIC;
-		bc[1] = ld_agent(&h->epoch);
+		const uint64_t tag = __hip_atomic_load(bin_tag(ws),
+		    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		bc[0] = (uint32_t)(tag >> 32) == NET2_BIN_MAGIC32 &&
+		    (uint32_t)tag != launch;
+		bc[1] = ld_agent(&ws[NET2_BIN_W_EPOCH]);
 	}
 	for (uint32_t b = threadIdx.x; b < NET2_SHA2_NBINS; b += blockDim.x)
 		cnt[b] = 0;
@@ -1985,12 +1917,23 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 			for (uint32_t w = threadIdx.x; w < 2 * BIN_CTL_PAR;
 			    w += blockDim.x)
 				ctl0[w] = 0;
-			if (threadIdx.x == 0)
-				h->epoch = 0;
+			if (threadIdx.x == 0) {
+				/* fresh memory (no re-init mark): its counters
+				 * are garbage, start them here */
+				const uint64_t tag = __hip_atomic_load(bin_tag(ws),
+				    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+				if ((uint32_t)(tag >> 32) != NET2_BIN_REINIT32)
+					for (int w = NET2_BIN_W_EPOCH + 1;
+					    w <= NET2_BIN_W_BINNED; w++)
+						ws[w] = 0;
+				ws[NET2_BIN_W_EPOCH] = 0;
+				add_agent(&ws[NET2_BIN_W_UNPREP], 1u);
+			}
 			__threadfence();
 			__syncthreads();
 			if (threadIdx.x == 0)
-				__hip_atomic_store(&h->magic, NET2_BIN_MAGIC,
+				__hip_atomic_store(bin_tag(ws),
+				    (uint64_t)NET2_BIN_MAGIC32 << 32 | launch,
 				    __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 		}
 		return;
@@ -2012,13 +1955,13 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 
 	/* 1: this workgroup's histogram; the ranks of its first tile's packets
 	 * kept in registers */
-	uint32_t bin0[NET2_BIN_ITEMS], rank0[NET2_BIN_ITEMS];
+	uint32_t bin0[kBinItems], rank0[kBinItems];
 	for (uint64_t t = blockIdx.x; t < ntiles; t += G) {
 		const uint64_t i0 = t * NET2_BIN_TILE + threadIdx.x;
 		if (t != blockIdx.x)
 			load_lens(lens, n, i0, len);
 #pragma unroll
-		for (int k = 0; k < NET2_BIN_ITEMS; k++) {
+		for (int k = 0; k < kBinItems; k++) {
 			const uint32_t bn = bin_of(len[k], blk_shift, lenbytes,
 			    NET2_SHA2_NBINS);
 			const uint32_t r = i0 + (uint64_t)k * 256 < n ?
@@ -2050,12 +1993,13 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		    __hip_atomic_fetch_add(&ctl[BIN_CTL_TOP], 1u, BIN_ORD,
 		    __HIP_MEMORY_SCOPE_AGENT) == ng - 1) {
 			/* every workgroup has read the epoch by now */
-			__hip_atomic_store(&h->epoch, bc[1] + 1, __ATOMIC_RELAXED,
-			    __HIP_MEMORY_SCOPE_AGENT);
+			__hip_atomic_store(&ws[NET2_BIN_W_EPOCH], bc[1] + 1,
+			    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 			uint32_t exp = BIN_UNDECIDED;
-			__hip_atomic_compare_exchange_strong(&ctl[BIN_CTL_STATE],
-			    &exp, (uint32_t)BIN_GO, BIN_ORD, __ATOMIC_RELAXED,
-			    __HIP_MEMORY_SCOPE_AGENT);
+			if (__hip_atomic_compare_exchange_strong(
+			    &ctl[BIN_CTL_STATE], &exp, (uint32_t)BIN_GO, BIN_ORD,
+			    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+				add_agent(&ws[NET2_BIN_W_BINNED], 1u);
 		}
 		BIN_STAMP(3);
 		const uint64_t t0 = wall_clock64();
@@ -2063,28 +2007,34 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		while ((st = ld_agent(&ctl[BIN_CTL_STATE])) == BIN_UNDECIDED) {
 			if (wall_clock64() - t0 > timeout) {
 				uint32_t exp = BIN_UNDECIDED;
-				__hip_atomic_compare_exchange_strong(
+				if (__hip_atomic_compare_exchange_strong(
 				    &ctl[BIN_CTL_STATE], &exp,
 				    (uint32_t)BIN_ABORT, BIN_ORD, __ATOMIC_RELAXED,
-				    __HIP_MEMORY_SCOPE_AGENT);
+				    __HIP_MEMORY_SCOPE_AGENT))
+					add_agent(&ws[NET2_BIN_W_ABORTS], 1u);
 			}
-			__builtin_amdgcn_s_sleep(NET2_BIN_SPIN_SLEEP);
+			__builtin_amdgcn_s_sleep(kBinSpinSleep);
 		}
 		BIN_STAMP(4);
 		bc[0] = st;
 	}
 	__syncthreads();
-	if (bc[0] == BIN_GO) {
+	bool binned = bc[0] == BIN_GO;
+	if (binned) {
 		/* 3: bin bases from the global histogram (8 bins per thread, a
 		 * shuffle scan per wave, the four wave totals) added to the
-		 * workgroup's starts, then its packets' places */
+		 * workgroup's starts, then its packets' places -- once the
+		 * histogram is known to add up to n */
 		constexpr int PER = NET2_SHA2_NBINS / 256;
 		const int lane = (int)__lane_id(), wave = (int)(threadIdx.x / 64);
 		uint32_t v[PER], sum = 0;
+		uint64_t sum64 = 0;
 #pragma unroll
 		for (int j = 0; j < PER; j++) {
+			const uint32_t c = ld_agent(&hist[threadIdx.x * PER + j]);
 			v[j] = sum;
-			sum += ld_agent(&hist[threadIdx.x * PER + j]);
+			sum += c;
+			sum64 += c;
 		}
 		uint32_t x = sum;
 #pragma unroll
@@ -2092,24 +2042,47 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 			const uint32_t y = __shfl_up(x, off);
 			if (lane >= off)
 				x += y;
+			sum64 += __shfl_xor(sum64, off);
 		}
 		if (lane == 63)
 			wsum[wave] = x;
+		if (lane == 0)
+			wtot[wave] = sum64;
 		__syncthreads();
 		uint32_t base = x - sum;
 		for (int w = 0; w < wave; w++)
 			base += wsum[w];
+		binned = wtot[0] + wtot[1] + wtot[2] + wtot[3] == n;
+		if (binned) {
 #pragma unroll
-		for (int j = 0; j < PER; j++)
-			start[threadIdx.x * PER + j] += base + v[j];
+			for (int j = 0; j < PER; j++)
+				start[threadIdx.x * PER + j] += base + v[j];
+			/* where the packets of at most two compressions start */
+			if (blockIdx.x == 0 && threadIdx.x == 255) {
+				ws[NET2_BIN_W_TAIL] = base + v[NET2_BIN_SHORT % PER];
+				ws[NET2_BIN_W_TAILID] = launch;
+			}
+		} else if (threadIdx.x == 0) {
+			/* the histogram is not this launch's alone: the hash
+			 * kernel of this launch ignores the order, and the next
+			 * launch re-initialises */
+			if (__hip_atomic_exchange(&ws[NET2_BIN_W_BAD], launch,
+			    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != launch)
+				add_agent(&ws[NET2_BIN_W_MISMATCH], 1u);
+			__hip_atomic_store(bin_tag(ws),
+			    (uint64_t)NET2_BIN_REINIT32 << 32, __ATOMIC_RELAXED,
+			    __HIP_MEMORY_SCOPE_AGENT);
+		}
 		__syncthreads();
 		BIN_STAMP(5);
+	}
+	if (binned) {
 		if (ntiles <= G) {
 			/* one tile: its packets' places from the kept ranks */
 			const uint64_t i0 = (uint64_t)blockIdx.x * NET2_BIN_TILE +
 			    threadIdx.x;
 #pragma unroll
-			for (int k = 0; k < NET2_BIN_ITEMS; k++) {
+			for (int k = 0; k < kBinItems; k++) {
 				const uint64_t i = i0 + (uint64_t)k * 256;
 				const uint32_t pos = start[bin0[k]] + rank0[k];
 				if (i < n && pos < n)
@@ -2126,7 +2099,7 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 				const uint64_t i0 = t * NET2_BIN_TILE + threadIdx.x;
 				load_lens(lens, n, i0, len);
 #pragma unroll
-				for (int k = 0; k < NET2_BIN_ITEMS; k++) {
+				for (int k = 0; k < kBinItems; k++) {
 					const uint64_t i = i0 + (uint64_t)k * 256;
 					if (i < n) {
 						const uint32_t pos = atomicAdd(
@@ -2141,27 +2114,27 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		BIN_STAMP(6);
 	} else {
 		bin_identity(perm, n, ntiles);
-		if (threadIdx.x == 0) {	/* re-initialise at the next launch */
-			__hip_atomic_store(&h->magic, 0ull, __ATOMIC_RELAXED,
+		if (bc[0] != BIN_GO && threadIdx.x == 0) {
+			/* ABORT: re-initialise at the next launch */
+			__hip_atomic_store(bin_tag(ws),
+			    (uint64_t)NET2_BIN_REINIT32 << 32, __ATOMIC_RELAXED,
 			    __HIP_MEMORY_SCOPE_AGENT);
 		}
 	}
 }
 
-/* Prepares a binning workspace so its first launch bins (one workgroup). */
+/* Prepares a binning workspace so its first launch bins, its counters
+ * zeroed (one workgroup). */
 __global__ __launch_bounds__(256) void bin_ws_init_kernel(uint32_t *ws)
 {
-	BinHdr *h = reinterpret_cast<BinHdr *>(ws);
-	for (uint32_t w = threadIdx.x; w < NET2_BIN_WS_WORDS - NET2_BIN_HDR;
+	for (uint32_t w = threadIdx.x; w < NET2_BIN_WS_WORDS - 2;
 	    w += blockDim.x)
-		ws[NET2_BIN_HDR + w] = 0;
-	if (threadIdx.x == 0)
-		h->epoch = 0;
+		ws[2 + w] = 0;
 	__threadfence();
 	__syncthreads();
 	if (threadIdx.x == 0)
-		__hip_atomic_store(&h->magic, NET2_BIN_MAGIC, __ATOMIC_RELEASE,
-		    __HIP_MEMORY_SCOPE_AGENT);
+		__hip_atomic_store(bin_tag(ws), (uint64_t)NET2_BIN_MAGIC32 << 32,
+		    __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 /* ---- host-side constant pad schedule ---------------------------------- */
@@ -2207,6 +2180,110 @@ static void pad_kw512(uint64_t bits, PadKW<uint64_t> &p)
 	}
 	for (int t = 0; t < 80; t++)
 		p.kw[t] = K512[t] + w[t];
+}
+
+/*
+ * The HMAC key blocks, once per launch on the host (RFC 2104 / FIPS 198-1:
+ * the ipad and opad chaining values after one compression of K' ^ ipad /
+ * K' ^ opad from the IV), in the word layout hmac_kernel's LDS copy takes.
+ * One SHA-256 / SHA-512 compression each (FIPS 180-4 6.2.2 / 6.4.2, the
+ * reference's SHA256Transform / SHA512Transform, src/sha2.c:374-445,
+ * :663-734): product code of the launcher, not the test oracle.
+ */
+static void h_compress256(uint32_t st[8], const uint32_t m[16])
+{
+	uint32_t w[64], v[8];
+	for (int t = 0; t < 16; t++)
+		w[t] = m[t];
+	for (int t = 16; t < 64; t++)
+		w[t] = w[t - 16] + (h_ror32(w[t - 15], 7) ^ h_ror32(w[t - 15], 18) ^
+		    (w[t - 15] >> 3)) + w[t - 7] + (h_ror32(w[t - 2], 17) ^
+		    h_ror32(w[t - 2], 19) ^ (w[t - 2] >> 10));
+	for (int i = 0; i < 8; i++)
+		v[i] = st[i];
+	for (int t = 0; t < 64; t++) {
+		const uint32_t t1 = v[7] + (h_ror32(v[4], 6) ^ h_ror32(v[4], 11) ^
+		    h_ror32(v[4], 25)) + ((v[4] & v[5]) ^ (~v[4] & v[6])) +
+		    K256[t] + w[t];
+		const uint32_t t2 = (h_ror32(v[0], 2) ^ h_ror32(v[0], 13) ^
+		    h_ror32(v[0], 22)) + ((v[0] & v[1]) ^ (v[0] & v[2]) ^
+		    (v[1] & v[2]));
+		for (int i = 7; i > 0; i--)
+			v[i] = v[i - 1];
+		v[4] += t1;
+		v[0] = t1 + t2;
+	}
+	for (int i = 0; i < 8; i++)
+		st[i] += v[i];
+}
+
+static void h_compress512(uint64_t st[8], const uint64_t m[16])
+{
+	uint64_t w[80], v[8];
+	for (int t = 0; t < 16; t++)
+		w[t] = m[t];
+	for (int t = 16; t < 80; t++)
+		w[t] = w[t - 16] + (h_ror64(w[t - 15], 1) ^ h_ror64(w[t - 15], 8) ^
+		    (w[t - 15] >> 7)) + w[t - 7] + (h_ror64(w[t - 2], 19) ^
+		    h_ror64(w[t - 2], 61) ^ (w[t - 2] >> 6));
+	for (int i = 0; i < 8; i++)
+		v[i] = st[i];
+	for (int t = 0; t < 80; t++) {
+		const uint64_t t1 = v[7] + (h_ror64(v[4], 14) ^ h_ror64(v[4], 18) ^
+		    h_ror64(v[4], 41)) + ((v[4] & v[5]) ^ (~v[4] & v[6])) +
+		    K512[t] + w[t];
+		const uint64_t t2 = (h_ror64(v[0], 28) ^ h_ror64(v[0], 34) ^
+		    h_ror64(v[0], 39)) + ((v[0] & v[1]) ^ (v[0] & v[2]) ^
+		    (v[1] & v[2]));
+		for (int i = 7; i > 0; i--)
+			v[i] = v[i - 1];
+		v[4] += t1;
+		v[0] = t1 + t2;
+	}
+	for (int i = 0; i < 8; i++)
+		st[i] += v[i];
+}
+
+/*
+ * ipad / opad midstates of key block kb (K' zero-padded to the block, at
+ * most 128 bytes) into hm->w[slot], hm->w[slot + 1].  halg: the SHA row
+ * (1 SHA-256, 2 SHA-384, 3 SHA-512).
+ */
+static void hmac_midstates(int halg, const uint8_t kb[128], HMid *hm,
+    int slot)
+{
+	for (int pass = 0; pass < 2; pass++) {
+		const uint8_t x = pass ? 0x5c : 0x36;
+		uint32_t *o = hm->w[slot + pass];
+		if (halg == 1) {
+			uint32_t st[8], m[16];
+			for (int i = 0; i < 8; i++)
+				st[i] = IV256[i];
+			for (int i = 0; i < 16; i++)
+				m[i] = (uint32_t)(kb[4 * i] ^ x) << 24 |
+				    (uint32_t)(kb[4 * i + 1] ^ x) << 16 |
+				    (uint32_t)(kb[4 * i + 2] ^ x) << 8 |
+				    (uint32_t)(kb[4 * i + 3] ^ x);
+			h_compress256(st, m);
+			for (int i = 0; i < 16; i++)
+				o[i] = i < 8 ? st[i] : 0u;
+		} else {
+			uint64_t st[8], m[16];
+			for (int i = 0; i < 8; i++)
+				st[i] = halg == 2 ? IV384[i] : IV512[i];
+			for (int i = 0; i < 16; i++) {
+				uint64_t v = 0;
+				for (int b = 0; b < 8; b++)
+					v = v << 8 | (uint8_t)(kb[8 * i + b] ^ x);
+				m[i] = v;
+			}
+			h_compress512(st, m);
+			for (int i = 0; i < 8; i++) {
+				o[2 * i] = (uint32_t)(st[i] >> 32);
+				o[2 * i + 1] = (uint32_t)st[i];
+			}
+		}
+	}
 }
 
 } /* namespace dev */
@@ -2269,23 +2346,83 @@ hipError_t net2_bin_ws_init(uint32_t *ws, hipStream_t s)
 	return hipGetLastError();
 }
 
+/*
+ * Binning limits: the grid cap (0: the device's co-resident capacity) and
+ * the barrier timeout in 100 MHz ticks, set by net2_sha2_bin_limits
+ * (diagnostics and tests; read once per launch from two atomics, no
+ * environment lookups on the launch path).
+ */
+static std::atomic<uint32_t> g_bin_grid_cap{0};
+static std::atomic<uint64_t> g_bin_timeout{NET2_BIN_TIMEOUT};
+
+void net2_bin_set_limits(uint32_t grid_cap, int64_t timeout_us)
+{
+	g_bin_grid_cap.store(grid_cap, std::memory_order_relaxed);
+	g_bin_timeout.store(timeout_us < 0 ? NET2_BIN_TIMEOUT :
+	    (uint64_t)timeout_us * 100, std::memory_order_relaxed);
+}
+
+/*
+ * The persistent grid's size: at most 256 workgroups and no more than the
+ * device can hold at once (workgroups per CU x CUs), cached per device --
+ * on a partitioned device (a CPX partition has 32 CUs) 256 workgroups need
+ * not all be resident, and the barrier would wait out its timeout on
+ * every launch.
+ */
+static uint32_t bin_resident_grid()
+{
+	static std::atomic<uint32_t> cache[64];
+	int dev = 0;
+	if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+		(void)hipGetLastError();
+		return NET2_BIN_GRID;
+	}
+	uint32_t g = cache[dev].load(std::memory_order_relaxed);
+	if (g != 0)
+		return g;
+	int per_cu = 0, cus = 0;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu,
+	    bin_onepass_kernel, 256, 0) != hipSuccess ||
+	    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
+	    dev) != hipSuccess || per_cu <= 0 || cus <= 0) {
+		(void)hipGetLastError();
+		g = 1;		/* one workgroup is always resident */
+	} else {
+		g = (uint32_t)std::min<int64_t>(NET2_BIN_GRID,
+		    (int64_t)per_cu * cus);
+	}
+	cache[dev].store(g, std::memory_order_relaxed);
+	return g;
+}
+
+/* A launch id for the binning and the hash kernel that reads its order:
+ * never 0 (the id of net2_bin_ws_init). */
+static uint32_t next_bin_launch()
+{
+	static std::atomic<uint32_t> seq{0};
+	uint32_t id;
+	do
+		id = seq.fetch_add(1, std::memory_order_relaxed) + 1;
+	while (id == 0);
+	return id;
+}
+
 /* Length-binned visiting order of a variable-length batch into ws. */
 hipError_t net2_bin_order(int alg, const uint32_t *lens, uint64_t n,
-    uint32_t *ws, hipStream_t s)
+    uint32_t *ws, hipStream_t s, uint32_t *launch)
 {
 	const bool s256 = alg == NET2_ALG_SHA256;
 	const int blk_shift = s256 ? 6 : 7;
 	const int lenbytes = s256 ? 8 : 16;
 	const uint64_t tiles = (n + NET2_BIN_TILE - 1) / NET2_BIN_TILE;
-	const unsigned g = (unsigned)(tiles < NET2_BIN_GRID ? tiles :
-	    NET2_BIN_GRID);
-	/* NET2_BIN_TIMEOUT_US (tests): the barrier's timeout, default 50 ms;
-	 * 0 exercises the ABORT path */
-	const char *e = getenv("NET2_BIN_TIMEOUT_US");
-	const uint64_t to = e != nullptr && *e != '\0' ?
-	    strtoull(e, nullptr, 10) * 100 : NET2_BIN_TIMEOUT;
+	uint32_t cap = bin_resident_grid();
+	const uint32_t forced = g_bin_grid_cap.load(std::memory_order_relaxed);
+	if (forced != 0 && forced < cap)
+		cap = forced;
+	const unsigned g = (unsigned)(tiles < cap ? tiles : cap);
+	*launch = next_bin_launch();
 	bin_onepass_kernel<<<g, 256, 0, s>>>(lens, n, blk_shift, lenbytes, ws,
-	    to);
+	    g_bin_timeout.load(std::memory_order_relaxed), *launch);
 	return hipGetLastError();
 }
 
@@ -2298,20 +2435,19 @@ hipError_t net2_launch_var(int alg, const uint8_t *base,
 	const bool s256 = alg == NET2_ALG_SHA256;
 	const int is384 = alg == NET2_ALG_SHA384;
 	const uint32_t dlen = s256 ? 32 : is384 ? 48 : 64;
-	uint32_t *perm = nullptr;
+	uint32_t launch = 0;
 
 	if (ws != nullptr) {
-		hipError_t e = net2_bin_order(alg, lens, n, ws, s);
+		hipError_t e = net2_bin_order(alg, lens, n, ws, s, &launch);
 		if (e != hipSuccess)
 			return e;
-		perm = ws + NET2_BIN_WS_WORDS;
 	}
 	if (s256)
 		var_kernel<Sha256V><<<grid_for(n), 256, 0, s>>>(base, offsets,
-		    lens, perm, n, out, dlen, 0);
+		    lens, ws, launch, n, out, dlen, 0);
 	else
 		var_kernel<Sha512V><<<grid_for(n), 256, 0, s>>>(base, offsets,
-		    lens, perm, n, out, dlen, is384);
+		    lens, ws, launch, n, out, dlen, is384);
 	return hipGetLastError();
 }
 /* H without the pair loop: the VERIFY kernel measured 1.5 % faster without
@@ -2322,29 +2458,46 @@ template <bool A, bool U, bool P> struct NoPair<Sha256T<A, U, P> > {
 	typedef Sha256T<A, U, false> type;
 };
 
-template <class H>
+template <class H, bool IS384>
 static void launch_hmac_var_mode(int mode, unsigned grid, hipStream_t s,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
-    const uint32_t *perm, uint64_t n, uint8_t *out, uint32_t dlen, int is384,
-    HKey<H::NW32> k, PadKW<typename H::word> pad, BurstArgs rx)
+    const uint32_t *ws, uint32_t launch, uint64_t n, uint8_t *out,
+    const HMid &hm, const PadKW<typename H::word> &pad, const BurstArgs &rx)
 {
 	if (mode == HMAC_SIGN)
-		hmac_kernel<H, false, HMAC_SIGN><<<grid, 256, 0, s>>>(base, offsets,
-		    lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx);
+		hmac_kernel<H, false, HMAC_SIGN, IS384><<<grid, 256, 0, s>>>(base,
+		    offsets, lens, ws, launch, 0, 0, n, out, hm, pad, rx);
 	else if (mode == HMAC_VERIFY)
-		hmac_kernel<typename NoPair<H>::type, false, HMAC_VERIFY>
-		    <<<grid, 256, 0, s>>>(base, offsets, lens, perm, 0, 0, n, out,
-		    dlen, is384, k, pad, rx);
+		hmac_kernel<typename NoPair<H>::type, false, HMAC_VERIFY, IS384>
+		    <<<grid, 256, 0, s>>>(base, offsets, lens, ws, launch, 0, 0, n,
+		    out, hm, pad, rx);
 	else if (mode == HMAC_BURST_RX)
-		hmac_kernel<typename NoPair<H>::type, false, HMAC_BURST_RX>
-		    <<<grid, 256, 0, s>>>(base, offsets, lens, perm, 0, 0, n, out,
-		    dlen, is384, k, pad, rx);
+		hmac_kernel<typename NoPair<H>::type, false, HMAC_BURST_RX, IS384>
+		    <<<grid, 256, 0, s>>>(base, offsets, lens, ws, launch, 0, 0, n,
+		    out, hm, pad, rx);
 	else if (mode == HMAC_BURST_TX)
-		hmac_kernel<H, false, HMAC_BURST_TX><<<grid, 256, 0, s>>>(base,
-		    offsets, lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx);
+		hmac_kernel<H, false, HMAC_BURST_TX, IS384><<<grid, 256, 0, s>>>(
+		    base, offsets, lens, ws, launch, 0, 0, n, out, hm, pad, rx);
 	else
-		hmac_kernel<H, false><<<grid, 256, 0, s>>>(base, offsets,
-		    lens, perm, 0, 0, n, out, dlen, is384, k, pad, rx);
+		hmac_kernel<H, false, HMAC_DIGESTS, IS384><<<grid, 256, 0, s>>>(
+		    base, offsets, lens, ws, launch, 0, 0, n, out, hm, pad, rx);
+}
+
+/* The fixed layout (offsets == NULL): digests only. */
+template <class H, bool IS384>
+static void launch_hmac_fixed(bool padconst, unsigned grid, hipStream_t s,
+    const uint8_t *base, uint64_t stride, uint32_t fixed_len, uint64_t n,
+    uint8_t *out, const HMid &hm, const PadKW<typename H::word> &pad,
+    const BurstArgs &rx)
+{
+	if (padconst)
+		hmac_kernel<H, true, HMAC_DIGESTS, IS384><<<grid, 256, 0, s>>>(
+		    base, nullptr, nullptr, nullptr, 0, stride, fixed_len, n, out,
+		    hm, pad, rx);
+	else
+		hmac_kernel<H, false, HMAC_DIGESTS, IS384><<<grid, 256, 0, s>>>(
+		    base, nullptr, nullptr, nullptr, 0, stride, fixed_len, n, out,
+		    hm, pad, rx);
 }
 
 hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
@@ -2357,62 +2510,71 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 	if ((mode == HMAC_BURST_RX || mode == HMAC_BURST_TX) !=
 	    (burst_args != nullptr))
 		return hipErrorInvalidValue;
+	if (burst_args != nullptr && burst_args->rec != nullptr &&
+	    mode != HMAC_BURST_TX)
+		return hipErrorInvalidValue;
 	const BurstArgs rx = burst_args ? *burst_args : BurstArgs{};
 	if (n == 0)
 		return hipSuccess;
 	const int halg = alg - 3;	/* HMAC row -> SHA row */
 	const bool s256 = halg == NET2_ALG_SHA256;
 	const int blk = s256 ? 64 : 128;
-	const int is384 = halg == NET2_ALG_SHA384;
-	const uint32_t dlen = s256 ? 32 : is384 ? 48 : 64;
+	const bool is384 = halg == NET2_ALG_SHA384;
 	uint8_t kb[128] = { 0 };
 	if (keylen > (size_t)blk)
 		return hipErrorInvalidValue;	/* registry keys are <= a block */
 	for (size_t i = 0; i < keylen; i++)
 		kb[i] = key[i];
-	uint32_t *perm = nullptr;
+	HMid hm = {};
+	hmac_midstates(halg, kb, &hm, 0);
+	if (mode == HMAC_BURST_RX && rx.alt) {
+		uint8_t ab[128] = { 0 };
+		for (int i = 0; i < 32; i++)	/* K' as big-endian words */
+			for (int b = 0; b < 4; b++)
+				ab[4 * i + b] = (uint8_t)(rx.altkey[i] >> (24 - 8 * b));
+		hmac_midstates(halg, ab, &hm, 2);
+	}
+	uint32_t launch = 0;
 	if (offsets != nullptr && ws != nullptr) {
-		hipError_t e = net2_bin_order(halg, lens, n, ws, s);
+		hipError_t e = net2_bin_order(halg, lens, n, ws, s, &launch);
 		if (e != hipSuccess)
 			return e;
-		perm = ws + NET2_BIN_WS_WORDS;
+	} else {
+		ws = nullptr;
 	}
 	const unsigned grid = grid_for(n);
 	const bool padconst = offsets == nullptr && fixed_len % blk == 0;
 	const uint64_t ibits = ((uint64_t)fixed_len + blk) << 3;
 	if (s256) {
-		HKey<16> k;
-		for (int i = 0; i < 16; i++)
-			k.w[i] = ((uint32_t)kb[4 * i] << 24) | ((uint32_t)kb[4 * i + 1] << 16) |
-			    ((uint32_t)kb[4 * i + 2] << 8) | kb[4 * i + 3];
 		PadKW<uint32_t> pad = {};
-		if (padconst) {
-			pad_kw256(ibits, pad);
-			hmac_kernel<Sha256H, true><<<grid, 256, 0, s>>>(base, offsets,
-			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad, rx);
-		} else if (offsets != nullptr) {
-			launch_hmac_var_mode<Sha256H>(mode, grid, s, base, offsets,
-			    lens, perm, n, out, dlen, 0, k, pad, rx);
+		if (offsets != nullptr) {
+			launch_hmac_var_mode<Sha256H, false>(mode, grid, s, base,
+			    offsets, lens, ws, launch, n, out, hm, pad, rx);
 		} else {
-			hmac_kernel<Sha256H, false><<<grid, 256, 0, s>>>(base, offsets,
-			    lens, perm, stride, fixed_len, n, out, dlen, 0, k, pad, rx);
+			if (padconst)
+				pad_kw256(ibits, pad);
+			launch_hmac_fixed<Sha256H, false>(padconst, grid, s, base,
+			    stride, fixed_len, n, out, hm, pad, rx);
 		}
 	} else {
-		HKey<32> k;
-		for (int i = 0; i < 32; i++)
-			k.w[i] = ((uint32_t)kb[4 * i] << 24) | ((uint32_t)kb[4 * i + 1] << 16) |
-			    ((uint32_t)kb[4 * i + 2] << 8) | kb[4 * i + 3];
 		PadKW<uint64_t> pad = {};
-		if (padconst) {
-			pad_kw512(ibits, pad);
-			hmac_kernel<Sha512HF, true><<<grid, 256, 0, s>>>(base, offsets,
-			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad, rx);
-		} else if (offsets != nullptr) {
-			launch_hmac_var_mode<Sha512H>(mode, grid, s, base, offsets,
-			    lens, perm, n, out, dlen, is384, k, pad, rx);
+		if (offsets != nullptr) {
+			if (is384)
+				launch_hmac_var_mode<Sha512H, true>(mode, grid, s, base,
+				    offsets, lens, ws, launch, n, out, hm, pad, rx);
+			else
+				launch_hmac_var_mode<Sha512H, false>(mode, grid, s,
+				    base, offsets, lens, ws, launch, n, out, hm, pad,
+				    rx);
 		} else {
-			hmac_kernel<Sha512HF, false><<<grid, 256, 0, s>>>(base, offsets,
-			    lens, perm, stride, fixed_len, n, out, dlen, is384, k, pad, rx);
+			if (padconst)
+				pad_kw512(ibits, pad);
+			if (is384)
+				launch_hmac_fixed<Sha512HF, true>(padconst, grid, s,
+				    base, stride, fixed_len, n, out, hm, pad, rx);
+			else
+				launch_hmac_fixed<Sha512HF, false>(padconst, grid, s,
+				    base, stride, fixed_len, n, out, hm, pad, rx);
 		}
 	}
 	return hipGetLastError();
@@ -2457,12 +2619,15 @@ hipError_t net2_launch_burst_prep(uint8_t *base, const uint64_t *offsets,
 
 hipError_t net2_launch_burst_final(uint64_t n, const uint8_t *status,
     const uint8_t *verdict, const uint32_t *seq, const uint32_t *flags,
-    uint32_t ivlen, uint8_t *iv, uint8_t *result, hipStream_t s)
+    uint32_t ivlen, uint8_t *iv, uint8_t *result, hipStream_t s,
+    uint32_t *seq_out, uint32_t *flags_out)
 {
-	if (ivlen > 64)
+	if (ivlen > 64 || (seq_out == nullptr) != (flags_out == nullptr))
 		return hipErrorInvalidValue;
+	if (n == 0)
+		return hipSuccess;
 	burst_final_kernel<<<grid_for(n), 256, 0, s>>>(n, status, verdict, seq,
-	    flags, ivlen, iv, result);
+	    flags, ivlen, iv, result, seq_out, flags_out);
 	return hipGetLastError();
 }
 

@@ -21,10 +21,23 @@
 
 /*
  * Binning workspace (uint32 words): a 16-word header (the one-pass
- * binning's state, sha2_kernels.hip bin_onepass_kernel), the histogram and
- * claim counters in two parities (2 x 2 x NBINS), then perm[n].
+ * binning's state, sha2_kernels.hip bin_onepass_kernel), the histogram in
+ * two parities (2 x NBINS), the barrier words (2 x NBINS, two parities and
+ * the probe stamps), then perm[n].  Header words:
  */
 #define NET2_BIN_HDR 16
+#define NET2_BIN_W_TAG 0	/* u64: magic << 32 | id of the launch that
+				 * prepared it (0: net2_bin_ws_init) */
+#define NET2_BIN_W_EPOCH 2	/* binned launches (selects the parity) */
+#define NET2_BIN_W_BAD 3	/* id of a launch whose order is unusable */
+#define NET2_BIN_W_ABORTS 4	/* barriers decided ABORT (timed out) */
+#define NET2_BIN_W_MISMATCH 5	/* launches whose histogram total was not n */
+#define NET2_BIN_W_UNPREP 6	/* launches that found the header unprepared */
+#define NET2_BIN_W_TAIL 7	/* last binned launch: first position of the
+				 * packets of at most 2 compressions ... */
+#define NET2_BIN_W_TAILID 8	/* ... and that launch's id */
+#define NET2_BIN_W_BINNED 9	/* barriers decided GO (since preparation by
+				 * net2_bin_ws_init) */
 /* header, the histogram's two parities, barrier words and probe stamps
  * (NET2_BIN_CTL, 4,096 words) */
 #define NET2_BIN_CTL (NET2_BIN_HDR + 2 * NET2_SHA2_NBINS)
@@ -42,13 +55,26 @@ hipError_t net2_launch_var(int alg, const uint8_t *base,
     const uint64_t *offsets, const uint32_t *lens, uint64_t n, uint8_t *out,
     uint32_t *ws, hipStream_t s);
 
-/* Prepare ws (>= NET2_BIN_WS_WORDS words) so its first binning bins; an
- * unprepared workspace hashes its first batch in submission order. */
+/* Prepare ws (>= NET2_BIN_WS_WORDS words) so its first binning bins, its
+ * counters zeroed; an unprepared workspace hashes its first batch in
+ * submission order. */
 hipError_t net2_bin_ws_init(uint32_t *ws, hipStream_t s);
 
-/* Length-binned order (ws as above; perm = ws + NET2_BIN_WS_WORDS). */
+/*
+ * Length-binned order (ws as above; perm = ws + NET2_BIN_WS_WORDS) under a
+ * fresh launch id (*launch), which the hash kernel reading the order must be
+ * given: it falls back to submission order when the binning found the
+ * workspace inconsistent (NET2_BIN_W_BAD).
+ */
 hipError_t net2_bin_order(int alg, const uint32_t *lens, uint64_t n,
-    uint32_t *ws, hipStream_t s);
+    uint32_t *ws, hipStream_t s, uint32_t *launch);
+
+/*
+ * Binning limits (net2_sha2_bin_limits): the persistent grid's size cap
+ * (0: the device's co-resident capacity, at most 256) and the grid
+ * barrier's timeout in microseconds (< 0: the default 50 ms).
+ */
+void net2_bin_set_limits(uint32_t grid_cap, int64_t timeout_us);
 
 /*
  * HMAC batch (alg = 4..6).  key/keylen in host memory (keylen <= block);
@@ -88,7 +114,12 @@ struct BurstArgs {
 	int alt_enc_set;
 	int no_cutoff;
 	uint32_t cutoff, rx_start;
-	uint32_t altkey[32];	/* K' as big-endian words */
+	uint32_t altkey[32];	/* K' as big-endian words (the launcher turns
+				 * it into midstates; unused by the kernel) */
+	/* TX: when set, header and hash field of datagram i go to
+	 * rec + i * (hashlen + 16) -- field at +0, header at +hashlen -- and
+	 * the datagrams in base are left as they are (the host burst path) */
+	uint8_t *rec;
 };
 hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
@@ -135,9 +166,12 @@ hipError_t net2_launch_burst_prep(uint8_t *base, const uint64_t *offsets,
     uint32_t hashlen, const uint32_t *seq_in, const uint32_t *flags_in,
     uint32_t *seq_out, uint32_t *flags_out, uint64_t *sub_off,
     uint32_t *sub_len, uint8_t *status, hipStream_t s);
+/* final: seq_out / flags_out (may be NULL) receive copies of the decoded
+ * headers (the host burst path: stores into mapped host memory) */
 hipError_t net2_launch_burst_final(uint64_t n, const uint8_t *status,
     const uint8_t *verdict, const uint32_t *seq, const uint32_t *flags,
-    uint32_t ivlen, uint8_t *iv, uint8_t *result, hipStream_t s);
+    uint32_t ivlen, uint8_t *iv, uint8_t *result, hipStream_t s,
+    uint32_t *seq_out = nullptr, uint32_t *flags_out = nullptr);
 
 /* Packet-header IVs (ivlen <= 64): out = n x ivlen bytes. */
 hipError_t net2_launch_ph_iv(const uint32_t *seq, const uint32_t *flags,

@@ -821,6 +821,81 @@ size_t small_device(const std::vector<int> &dv)
 	return 0;
 }
 
+/*
+ * Shards a host-memory batch of n packets over the devices (net2_sha2_batch,
+ * the host packet bursts): contiguous slices -- by packet count for the
+ * fixed layout (lens == NULL), by bytes otherwise -- no slice under
+ * slice_min_bytes() of payload, one host thread per extra device.  The
+ * device list starts at the caller's current device, so one process per GPU
+ * with max_devices == 1 stays on its own device.  fn(didx, ordinal, lo, hi)
+ * runs one slice; the first error is returned.
+ */
+template <class F>
+int shard_batch(uint64_t n, const uint32_t *lens, uint32_t fixed_len,
+    int max_devices, const F &fn)
+{
+	const std::vector<int> dv = batch_devices();
+	if (dv.empty())
+		return ENODEV;
+	size_t nd = dv.size();
+	if (max_devices > 0 && (size_t)max_devices < nd)
+		nd = (size_t)max_devices;
+	if ((uint64_t)nd > n)
+		nd = (size_t)n;
+	uint64_t total = 0;
+	if (lens == nullptr) {
+		total = n * (uint64_t)fixed_len;
+	} else {
+		for (uint64_t i = 0; i < n; i++)
+			total += lens[i];
+	}
+	const uint64_t min_slice = slice_min_bytes();
+	if (min_slice > 0 && nd > 1)
+		nd = (size_t)std::max<uint64_t>(1, std::min<uint64_t>(nd,
+		    total / min_slice));
+
+	/* Contiguous slices: by packet count, or by bytes for var layout. */
+	std::vector<uint64_t> cut(nd + 1, 0);
+	cut[nd] = n;
+	if (lens == nullptr) {
+		for (size_t d = 1; d < nd; d++)
+			cut[d] = n * d / nd;
+	} else {
+		uint64_t acc = 0;
+		size_t d = 1;
+		for (uint64_t i = 0; i < n && d < nd; i++) {
+			acc += lens[i];
+			while (d < nd && acc * nd >= total * d)
+				cut[d++] = i + 1;
+		}
+		for (; d < nd; d++)
+			cut[d] = n;
+	}
+
+	int prev = -1;
+	(void)hipGetDevice(&prev);
+	size_t first = 0;
+	for (size_t d = 0; d < dv.size(); d++)
+		if (dv[d] == prev)
+			first = d;
+	std::vector<int> rcs(nd, 0);
+	std::vector<std::thread> th;
+	for (size_t d = 1; d < nd; d++)
+		th.emplace_back([&, d]() {
+			const size_t e = (first + d) % dv.size();
+			rcs[d] = fn(e, dv[e], cut[d], cut[d + 1]);
+		});
+	rcs[0] = fn(first, dv[first], cut[0], cut[1]);
+	for (std::thread &t : th)
+		t.join();
+	if (prev >= 0)
+		(void)hipSetDevice(prev);
+	for (int r : rcs)
+		if (r != 0)
+			return r;
+	return 0;
+}
+
 } /* namespace */
 
 int net2_co_run(const net2co::Request &r)
@@ -921,6 +996,34 @@ NET2_EXPORT int net2_sha2_workspace_init(void *d_ws, size_t ws_bytes,
 	return 0;
 }
 
+NET2_EXPORT int net2_sha2_bin_limits(uint32_t grid_cap, int64_t timeout_us)
+{
+	net2_bin_set_limits(grid_cap, timeout_us);
+	return 0;
+}
+
+NET2_EXPORT int net2_sha2_workspace_stats(const void *d_ws, size_t ws_bytes,
+    struct net2_bin_stats *st)
+{
+	if (d_ws == nullptr || st == nullptr ||
+	    ws_bytes < net2_sha2_dev_var_workspace(0) ||
+	    ((uintptr_t)d_ws & 7) != 0)
+		return EINVAL;
+	int rc = check_current_device();
+	if (rc != 0)
+		return rc;
+	uint32_t h[NET2_BIN_HDR];
+	HIP_TRY(hipMemcpy(h, d_ws, sizeof(h), hipMemcpyDeviceToHost));
+	const uint64_t tag = (uint64_t)h[NET2_BIN_W_TAG + 1] << 32 |
+	    h[NET2_BIN_W_TAG];
+	st->prepared = (uint32_t)(tag >> 32) == 0x4e324253u;	/* "N2BS" */
+	st->binned = h[NET2_BIN_W_BINNED];
+	st->aborts = h[NET2_BIN_W_ABORTS];
+	st->mismatches = h[NET2_BIN_W_MISMATCH];
+	st->unprepared = h[NET2_BIN_W_UNPREP];
+	return 0;
+}
+
 NET2_EXPORT int net2_sha2_dev_var(int alg, const void *d_base,
     const uint64_t *d_offsets, const uint32_t *d_lens, uint64_t n,
     void *d_digests, void *d_ws, size_t ws_bytes, void *stream)
@@ -956,72 +1059,13 @@ NET2_EXPORT int net2_sha2_batch(int alg, const void *base,
 		return EINVAL;
 	if (offsets == nullptr && n > 1 && stride < fixed_len)
 		return EINVAL;
-	const std::vector<int> dv = batch_devices();
-	if (dv.empty())
-		return ENODEV;
-	size_t nd = dv.size();
-	if (max_devices > 0 && (size_t)max_devices < nd)
-		nd = (size_t)max_devices;
-	if ((uint64_t)nd > n)
-		nd = (size_t)n;
-	uint64_t total = 0;
-	if (offsets == nullptr) {
-		total = n * (uint64_t)fixed_len;
-	} else {
-		for (uint64_t i = 0; i < n; i++)
-			total += lens[i];
-	}
-	const uint64_t min_slice = slice_min_bytes();
-	if (min_slice > 0 && nd > 1)
-		nd = (size_t)std::max<uint64_t>(1, std::min<uint64_t>(nd,
-		    total / min_slice));
-
-	/* Contiguous slices: by packet count, or by bytes for var layout. */
-	std::vector<uint64_t> cut(nd + 1, 0);
-	cut[nd] = n;
-	if (offsets == nullptr) {
-		for (size_t d = 1; d < nd; d++)
-			cut[d] = n * d / nd;
-	} else {
-		uint64_t acc = 0;
-		size_t d = 1;
-		for (uint64_t i = 0; i < n && d < nd; i++) {
-			acc += lens[i];
-			while (d < nd && acc * nd >= total * d)
-				cut[d++] = i + 1;
-		}
-		for (; d < nd; d++)
-			cut[d] = n;
-	}
-
-	/* Device list starts at the caller's current device, so one process
-	 * per GPU with max_devices == 1 stays on its own device. */
-	int prev = -1;
-	(void)hipGetDevice(&prev);
-	size_t first = 0;
-	for (size_t d = 0; d < dv.size(); d++)
-		if (dv[d] == prev)
-			first = d;
-	std::vector<int> rcs(nd, 0);
-	std::vector<std::thread> th;
-	for (size_t d = 1; d < nd; d++)
-		th.emplace_back([&, d]() {
-			const size_t e = (first + d) % dv.size();
-			rcs[d] = run_device_slice(e, dv[e], alg,
-			    (const uint8_t *)base, offsets, lens, stride,
-			    fixed_len, cut[d], cut[d + 1], (uint8_t *)digests);
-		});
-	rcs[0] = run_device_slice(first, dv[first], alg, (const uint8_t *)base,
-	    offsets, lens, stride, fixed_len, cut[0], cut[1],
-	    (uint8_t *)digests);
-	for (std::thread &t : th)
-		t.join();
-	if (prev >= 0)
-		(void)hipSetDevice(prev);
-	for (int r : rcs)
-		if (r != 0)
-			return r;
-	return 0;
+	return shard_batch(n, offsets != nullptr ? lens : nullptr, fixed_len,
+	    max_devices, [&](size_t didx, int ordinal, uint64_t lo,
+	    uint64_t hi) {
+		return run_device_slice(didx, ordinal, alg,
+		    (const uint8_t *)base, offsets, lens, stride, fixed_len,
+		    lo, hi, (uint8_t *)digests);
+	});
 }
 
 NET2_EXPORT int net2_sha2_numa_stats(int device, int *numa_node,
@@ -1321,8 +1365,10 @@ NET2_EXPORT int net2_ph_to_iv_dev(const uint32_t *d_seq,
 namespace {
 
 /* Workspace of a burst, carved in this order, every piece 16-byte aligned:
- * region offsets and lengths for the HMAC kernel, status and verdict bytes,
- * decoded headers, the binning scratch. */
+ * the binning scratch first -- its header and histograms at offset 0 for
+ * every n, so one workspace serves bursts of any size up to its own and
+ * net2_sha2_workspace_init / _stats apply to it -- then region offsets and
+ * lengths for the prep kernel, status and verdict bytes, decoded headers. */
 struct BurstWs {
 	uint64_t *sub_off;
 	uint32_t *sub_len;
@@ -1344,13 +1390,13 @@ size_t burst_layout(uint64_t n, uint8_t *base, BurstWs *w)
 		at += a16(bytes);
 		return p;
 	};
+	uint32_t *bn = (uint32_t *)take(((size_t)NET2_BIN_WS_WORDS + n) * 4);
 	uint64_t *so = (uint64_t *)take(8 * n);
 	uint32_t *sl = (uint32_t *)take(4 * n);
 	uint8_t *st = take(n);
 	uint8_t *vd = take(n);
 	uint32_t *sq = (uint32_t *)take(4 * n);
 	uint32_t *fl = (uint32_t *)take(4 * n);
-	uint32_t *bn = (uint32_t *)take(((size_t)NET2_BIN_WS_WORDS + n) * 4);
 	if (w != nullptr)
 		*w = { so, sl, st, vd, sq, fl, bn };
 	return at;
@@ -1381,39 +1427,24 @@ int check_burst_args(int hash_alg, const void *key, size_t keylen,
 	return check_current_device();
 }
 
-}	/* namespace */
-
-NET2_EXPORT size_t net2_packet_burst_workspace(uint64_t n)
+/*
+ * The hash steps of net2_packet_decode for a device-resident burst.
+ * hdr_out: d_seq / d_flags are copies the final kernel makes (the host
+ * path: mapped host memory) -- the HMAC kernel keeps the decoded headers in
+ * the workspace; otherwise they are where the HMAC kernel decodes to.
+ */
+int decode_burst(const struct net2_burst_rx_keys *k, uint32_t ivlen,
+    const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
+    uint64_t n, uint8_t *d_result, void *d_iv, uint32_t *d_seq,
+    uint32_t *d_flags, void *d_ws, hipStream_t s, bool hdr_out)
 {
-	return burst_layout(n, nullptr, nullptr);
-}
-
-NET2_EXPORT int net2_packet_decode_burst_ck(const struct net2_burst_rx_keys *k,
-    uint32_t ivlen, const void *d_base, const uint64_t *d_offsets,
-    const uint32_t *d_lens, uint64_t n, uint8_t *d_result, void *d_iv,
-    uint32_t *d_seq, uint32_t *d_flags, void *d_ws, size_t ws_bytes,
-    void *stream)
-{
-	if (k == nullptr)
-		return EINVAL;
 	const int hash_alg = k->hash_alg;
-	int rc = check_burst_args(hash_alg, k->hash_key, k->hash_keylen, ivlen,
-	    d_base, d_offsets, d_lens, n, d_result, d_ws, ws_bytes);
-	if (rc != 0)
-		return rc;
-	/* an alternate key is new key material under the same algorithms */
 	const int hash_set = hash_alg != NET2_HASH_NIL;
 	const bool alt = hash_set && k->alt_hash_key != nullptr;
-	if (alt && k->alt_hash_keylen != k->hash_keylen)
-		return EINVAL;
-	if (n == 0)
-		return 0;
-	if ((d_seq == nullptr) != (d_flags == nullptr))
-		return EINVAL;
 	BurstWs w;
 	burst_layout(n, (uint8_t *)d_ws, &w);
-	uint32_t *seq = d_seq ? d_seq : w.seq, *flags = d_flags ? d_flags : w.flags;
-	hipStream_t s = (hipStream_t)stream;
+	uint32_t *seq = d_seq && !hdr_out ? d_seq : w.seq;
+	uint32_t *flags = d_flags && !hdr_out ? d_flags : w.flags;
 	const int enc_set = k->enc_alg != 0;
 	if (hash_set) {
 		/* header decode, key choice, flag checks and HMAC verify in one
@@ -1442,8 +1473,77 @@ NET2_EXPORT int net2_packet_decode_burst_ck(const struct net2_burst_rx_keys *k,
 		    flags, w.sub_off, w.sub_len, w.status, s));
 	}
 	HIP_TRY(net2_launch_burst_final(n, w.status, w.verdict, seq, flags,
-	    enc_set ? ivlen : 0, (uint8_t *)d_iv, d_result, s));
+	    enc_set ? ivlen : 0, (uint8_t *)d_iv, d_result, s,
+	    hdr_out ? d_seq : nullptr, hdr_out ? d_flags : nullptr));
 	return 0;
+}
+
+/*
+ * The hash steps of net2_packet_encode for a device-resident burst.  rec
+ * (keyed hash only): header and hash field of every datagram to a record of
+ * their own (BurstArgs::rec) instead of into d_base.
+ */
+int encode_burst(int hash_alg, const void *hash_key, size_t hash_keylen,
+    int enc_alg, const uint32_t *d_seq, const uint32_t *d_flags,
+    void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
+    uint64_t n, uint8_t *d_result, void *d_ws, hipStream_t s, uint8_t *rec)
+{
+	BurstWs w;
+	burst_layout(n, (uint8_t *)d_ws, &w);
+	if (hash_alg != NET2_HASH_NIL) {
+		/* flag and room checks, header write and HMAC sign in one
+		 * kernel over the wire datagrams; the TX code is final (no
+		 * verdict to fold in), so the kernel writes it to d_result */
+		BurstArgs tx = {};
+		tx.seq = const_cast<uint32_t *>(d_seq);
+		tx.flags = const_cast<uint32_t *>(d_flags);
+		tx.status = d_result;
+		tx.enc_set = enc_alg != 0;
+		tx.rec = rec;
+		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)hash_key,
+		    hash_keylen, (const uint8_t *)d_base, d_offsets, d_lens, 0,
+		    0, n, (uint8_t *)d_base, w.bin, s, NET2_HMAC_MODE_BURST_TX,
+		    &tx));
+		return 0;
+	}
+	HIP_TRY(net2_launch_burst_prep((uint8_t *)d_base, d_offsets,
+	    d_lens, n, 1, 0, enc_alg != 0, 0, d_seq, d_flags, nullptr,
+	    nullptr, w.sub_off, w.sub_len, w.status, s));
+	HIP_TRY(net2_launch_burst_final(n, w.status, nullptr, d_seq, d_flags, 0,
+	    nullptr, d_result, s));
+	return 0;
+}
+
+}	/* namespace */
+
+NET2_EXPORT size_t net2_packet_burst_workspace(uint64_t n)
+{
+	return burst_layout(n, nullptr, nullptr);
+}
+
+NET2_EXPORT int net2_packet_decode_burst_ck(const struct net2_burst_rx_keys *k,
+    uint32_t ivlen, const void *d_base, const uint64_t *d_offsets,
+    const uint32_t *d_lens, uint64_t n, uint8_t *d_result, void *d_iv,
+    uint32_t *d_seq, uint32_t *d_flags, void *d_ws, size_t ws_bytes,
+    void *stream)
+{
+	if (k == nullptr)
+		return EINVAL;
+	int rc = check_burst_args(k->hash_alg, k->hash_key, k->hash_keylen,
+	    ivlen, d_base, d_offsets, d_lens, n, d_result, d_ws, ws_bytes);
+	if (rc != 0)
+		return rc;
+	/* an alternate key is new key material under the same algorithms */
+	const bool alt = k->hash_alg != NET2_HASH_NIL &&
+	    k->alt_hash_key != nullptr;
+	if (alt && k->alt_hash_keylen != k->hash_keylen)
+		return EINVAL;
+	if (n == 0)
+		return 0;
+	if ((d_seq == nullptr) != (d_flags == nullptr))
+		return EINVAL;
+	return decode_burst(k, ivlen, d_base, d_offsets, d_lens, n, d_result,
+	    d_iv, d_seq, d_flags, d_ws, (hipStream_t)stream, false);
 }
 
 NET2_EXPORT int net2_packet_decode_burst(int hash_alg, const void *hash_key,
@@ -1473,31 +1573,414 @@ NET2_EXPORT int net2_packet_encode_burst(int hash_alg, const void *hash_key,
 		return rc;
 	if (d_seq == nullptr || d_flags == nullptr)
 		return EINVAL;
-	BurstWs w;
-	burst_layout(n, (uint8_t *)d_ws, &w);
-	hipStream_t s = (hipStream_t)stream;
-	const int hash_set = hash_alg != NET2_HASH_NIL;
-	if (hash_set) {
-		/* flag and room checks, header write and HMAC sign in one
-		 * kernel over the wire datagrams; the TX code is final (no
-		 * verdict to fold in), so the kernel writes it to d_result */
-		BurstArgs tx = {};
-		tx.seq = const_cast<uint32_t *>(d_seq);
-		tx.flags = const_cast<uint32_t *>(d_flags);
-		tx.status = d_result;
-		tx.enc_set = enc_alg != 0;
-		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)hash_key,
-		    hash_keylen, (const uint8_t *)d_base, d_offsets, d_lens, 0,
-		    0, n, (uint8_t *)d_base, w.bin, s, NET2_HMAC_MODE_BURST_TX,
-		    &tx));
-		return 0;
-	} else {
-		HIP_TRY(net2_launch_burst_prep((uint8_t *)d_base, d_offsets,
-		    d_lens, n, 1, 0, enc_alg != 0, 0, d_seq, d_flags, nullptr,
-		    nullptr, w.sub_off, w.sub_len, w.status, s));
+	return encode_burst(hash_alg, hash_key, hash_keylen, enc_alg, d_seq,
+	    d_flags, d_base, d_offsets, d_lens, n, d_result, d_ws,
+	    (hipStream_t)stream, nullptr);
+}
+
+/* ---- packet bursts from host memory ----------------------------------------- */
+
+namespace {
+
+/*
+ * One pipeline slot of the host burst path: pinned staging for the packed
+ * datagrams, their offsets / lengths and (TX) headers, pinned staging for
+ * results bound for pageable memory, the device copies and the burst
+ * workspace, a stream.  Two slots per device double-buffer pack / H2D /
+ * kernels / copy-back, as Slot does for digests.
+ */
+struct BurstSlot {
+	hipStream_t stream = nullptr;
+	hipEvent_t done = nullptr;
+	bool busy = false;
+	uint8_t *h_in = nullptr, *h_out = nullptr;
+	uint64_t *h_off = nullptr;
+	uint32_t *h_len = nullptr, *h_hdr = nullptr;
+	uint8_t *d_in = nullptr, *d_ws = nullptr;
+	uint64_t *d_off = nullptr;
+	uint32_t *d_len = nullptr, *d_hdr = nullptr;
+	size_t cap_in = 0, cap_n = 0;
+	/* run once the chunk's kernels are done: results to the caller */
+	std::function<int()> finish;
+
+	/* results staged per datagram: RX code + IV (<= 64) + header; TX code
+	 * + record (hash field + header, <= 80) */
+	static size_t out_bytes(size_t n)
+	{
+		return n * 81 + 256;
 	}
-	HIP_TRY(net2_launch_burst_final(n, w.status, nullptr, d_seq, d_flags, 0,
-	    nullptr, d_result, s));
+
+	void release()
+	{
+		if (h_in) (void)hipHostFree(h_in);
+		if (h_out) (void)hipHostFree(h_out);
+		if (h_off) (void)hipHostFree(h_off);
+		if (h_len) (void)hipHostFree(h_len);
+		if (h_hdr) (void)hipHostFree(h_hdr);
+		if (d_in) (void)hipFree(d_in);
+		if (d_ws) (void)hipFree(d_ws);
+		if (d_off) (void)hipFree(d_off);
+		if (d_len) (void)hipFree(d_len);
+		if (d_hdr) (void)hipFree(d_hdr);
+		h_in = h_out = nullptr;
+		h_off = nullptr;
+		h_len = h_hdr = nullptr;
+		d_in = d_ws = nullptr;
+		d_off = nullptr;
+		d_len = d_hdr = nullptr;
+		cap_in = cap_n = 0;
+	}
+
+	int reserve(size_t in, size_t n)
+	{
+		if (stream == nullptr) {
+			HIP_TRY(hipStreamCreateWithFlags(&stream,
+			    hipStreamNonBlocking));
+			HIP_TRY(hipEventCreateWithFlags(&done,
+			    hipEventDisableTiming));
+		}
+		if (in <= cap_in && n <= cap_n)
+			return 0;
+		in = std::max<size_t>({in + in / 8, cap_in, 4096});
+		n = std::max<size_t>({n + n / 4, cap_n, 64});
+		release();
+		HIP_TRY(hipHostMalloc((void **)&h_in, in, hipHostMallocDefault));
+		HIP_TRY(hipHostMalloc((void **)&h_out, out_bytes(n),
+		    hipHostMallocDefault));
+		HIP_TRY(hipHostMalloc((void **)&h_off, n * 8,
+		    hipHostMallocDefault));
+		HIP_TRY(hipHostMalloc((void **)&h_len, n * 4,
+		    hipHostMallocDefault));
+		HIP_TRY(hipHostMalloc((void **)&h_hdr, n * 8,
+		    hipHostMallocDefault));
+		HIP_TRY(hipMalloc((void **)&d_in, in));
+		HIP_TRY(hipMalloc((void **)&d_off, n * 8));
+		HIP_TRY(hipMalloc((void **)&d_len, n * 4));
+		HIP_TRY(hipMalloc((void **)&d_hdr, n * 8));
+		HIP_TRY(hipMalloc((void **)&d_ws, burst_layout(n, nullptr,
+		    nullptr)));
+		/* its binning area prepared once, so the first chunk bins */
+		HIP_TRY(net2_bin_ws_init((uint32_t *)d_ws, nullptr));
+		HIP_TRY(hipStreamSynchronize(nullptr));
+		cap_in = in;
+		cap_n = n;
+		return 0;
+	}
+
+	int drain()
+	{
+		if (!busy)
+			return 0;
+		busy = false;
+		HIP_TRY(hipEventSynchronize(done));
+		std::function<int()> f;
+		f.swap(finish);
+		return f ? f() : 0;
+	}
+};
+
+struct BurstCtx {
+	std::mutex mu;		/* one host burst per device at a time */
+	BurstSlot slot[2];
+};
+
+std::mutex g_bctx_mu;
+std::vector<std::unique_ptr<BurstCtx>> g_bctx;
+
+BurstCtx *bctx_for(size_t idx)
+{
+	std::lock_guard<std::mutex> g(g_bctx_mu);
+	if (g_bctx.size() <= idx)
+		g_bctx.resize(idx + 1);
+	if (!g_bctx[idx])
+		g_bctx[idx].reset(new BurstCtx());
+	return g_bctx[idx].get();
+}
+
+/*
+ * Where the kernels store a chunk's output of `bytes` bytes bound for the
+ * caller's `user` (its chunk slice): straight into it through its device
+ * mapping when it is page-locked, else into `stage` (the slot's pinned
+ * results, mapped) -- then *copy is set and the caller copies it over once
+ * the chunk is done.
+ */
+uint8_t *out_ptr(void *user, bool user_pinned, uint8_t *stage, bool *copy)
+{
+	void *dp = nullptr;
+	*copy = false;
+	if (user_pinned && hipHostGetDevicePointer(&dp, user, 0) == hipSuccess &&
+	    dp != nullptr)
+		return (uint8_t *)dp;
+	(void)hipGetLastError();
+	if (hipHostGetDevicePointer(&dp, stage, 0) == hipSuccess && dp != nullptr) {
+		*copy = true;
+		return (uint8_t *)dp;
+	}
+	(void)hipGetLastError();
+	return nullptr;
+}
+
+/* The pinned state of each caller buffer of a host burst (looked up once). */
+struct BurstPins {
+	bool result = false, iv = false, seq = false, flags = false;
+};
+
+/* What a host burst is asked to do; pointers are the caller's. */
+struct HostBurst {
+	bool tx;
+	/* RX */
+	const struct net2_burst_rx_keys *keys;
+	uint32_t ivlen;
+	void *iv;
+	uint32_t *seq_out, *flags_out;
+	/* TX */
+	int hash_alg;
+	const void *hash_key;
+	size_t hash_keylen;
+	int enc_alg;
+	const uint32_t *seq_in, *flags_in;
+	/* both */
+	uint8_t *base;
+	const uint64_t *offsets;
+	const uint32_t *lens;
+	uint8_t *result;
+};
+
+/* Chunk [lo, hi) of a host burst into slot s. */
+int enqueue_burst_chunk(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
+    const BurstPins &pins, uint64_t lo, uint64_t hi)
+{
+	const uint64_t n = hi - lo;
+	const PackPlan plan = pack_sizes(pool, hb.lens + lo, n);
+	const size_t bytes = plan.start[plan.nt];
+	int rc;
+	if ((rc = s.reserve(bytes, n)) != 0)
+		return rc;
+	pack_fill(pool, plan, s.h_in, s.h_off, s.h_len, hb.base, hb.offsets + lo,
+	    hb.lens + lo, n);
+	if (bytes != 0)
+		HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
+		    hipMemcpyHostToDevice, s.stream));
+	HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, n * 8, hipMemcpyHostToDevice,
+	    s.stream));
+	HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, n * 4, hipMemcpyHostToDevice,
+	    s.stream));
+
+	/* staged results: [code n][IV n x ivlen | records][seq n][flags n] */
+	uint8_t *st_res = s.h_out;
+	uint8_t *st_b = st_res + a16(n);
+	bool c_res, c_iv = false, c_seq = false, c_fl = false;
+	uint8_t *k_res = out_ptr(hb.result + lo, pins.result, st_res, &c_res);
+	if (k_res == nullptr)
+		return EIO;
+	std::vector<std::function<void()>> copies;
+	if (!hb.tx) {
+		const uint32_t ivlen = hb.keys->enc_alg != 0 ? hb.ivlen : 0;
+		uint8_t *st_iv = st_b;
+		uint8_t *st_sq = st_iv + a16((size_t)n * ivlen);
+		uint8_t *st_fl = st_sq + a16((size_t)n * 4);
+		uint8_t *k_iv = nullptr, *k_sq = nullptr, *k_fl = nullptr;
+		if (hb.iv != nullptr && ivlen > 0 &&
+		    (k_iv = out_ptr((uint8_t *)hb.iv + lo * ivlen, pins.iv, st_iv,
+		    &c_iv)) == nullptr)
+			return EIO;
+		if (hb.seq_out != nullptr &&
+		    ((k_sq = out_ptr(hb.seq_out + lo, pins.seq, st_sq, &c_seq)) ==
+		    nullptr || (k_fl = out_ptr(hb.flags_out + lo, pins.flags,
+		    st_fl, &c_fl)) == nullptr))
+			return EIO;
+		if ((rc = decode_burst(hb.keys, hb.ivlen, s.d_in, s.d_off, s.d_len,
+		    n, k_res, k_iv, (uint32_t *)k_sq, (uint32_t *)k_fl, s.d_ws,
+		    s.stream, true)) != 0)
+			return rc;
+		if (c_iv)
+			copies.push_back([=]() { memcpy((uint8_t *)hb.iv +
+			    lo * ivlen, st_iv, (size_t)n * ivlen); });
+		if (c_seq)
+			copies.push_back([=]() { memcpy(hb.seq_out + lo, st_sq,
+			    (size_t)n * 4); });
+		if (c_fl)
+			copies.push_back([=]() { memcpy(hb.flags_out + lo, st_fl,
+			    (size_t)n * 4); });
+	} else {
+		memcpy(s.h_hdr, hb.seq_in + lo, (size_t)n * 4);
+		memcpy(s.h_hdr + n, hb.flags_in + lo, (size_t)n * 4);
+		HIP_TRY(hipMemcpyAsync(s.d_hdr, s.h_hdr, n * 8,
+		    hipMemcpyHostToDevice, s.stream));
+		const bool keyed = hb.hash_alg != NET2_HASH_NIL;
+		void *recd = nullptr;
+		if (keyed && (hipHostGetDevicePointer(&recd, st_b, 0) != hipSuccess ||
+		    recd == nullptr)) {
+			(void)hipGetLastError();
+			return EIO;
+		}
+		if ((rc = encode_burst(hb.hash_alg, hb.hash_key, hb.hash_keylen,
+		    hb.enc_alg, s.d_hdr, s.d_hdr + n, s.d_in, s.d_off, s.d_len, n,
+		    k_res, s.d_ws, s.stream, (uint8_t *)recd)) != 0)
+			return rc;
+	}
+	HIP_TRY(hipEventRecord(s.done, s.stream));
+	s.busy = true;
+	const bool tx = hb.tx;
+	const int dl = tx && hb.hash_alg != NET2_HASH_NIL ?
+	    digest_len(hb.hash_alg) : 0;
+	WorkPool *pp = &pool;
+	s.finish = [=]() {
+		if (c_res)
+			memcpy(hb.result + lo, st_res, (size_t)n);
+		for (const std::function<void()> &c : copies)
+			c();
+		if (!tx)
+			return 0;
+		/* TX: the sealed header (and hash field) of every OK datagram
+		 * into the caller's slot (packet.n2t:384-392, :417-427) */
+		const size_t nt = std::min<size_t>(kPackThreads,
+		    std::max<size_t>(1, n >> 13));
+		pp->run(nt, [=](size_t t) {
+			for (uint64_t j = n * t / nt; j < n * (t + 1) / nt; j++) {
+				if (hb.result[lo + j] != NET2_PENCODE_OK)
+					continue;
+				uint8_t *dg = hb.base + hb.offsets[lo + j];
+				if (dl != 0) {
+					const uint8_t *r = st_b + j * (dl + 16);
+					memcpy(dg, r + dl, 8);
+					memcpy(dg + 8, r, dl);
+				} else {
+					const uint32_t sq = hb.seq_in[lo + j];
+					const uint32_t fl = hb.flags_in[lo + j];
+					for (int b = 0; b < 4; b++) {
+						dg[b] = (uint8_t)(sq >> (24 - 8 * b));
+						dg[4 + b] = (uint8_t)(fl >> (24 - 8 * b));
+					}
+				}
+			}
+		});
+		return 0;
+	};
 	return 0;
 }
 
+/* One device's share [lo, hi) of a host burst, chunked and double-buffered. */
+int run_burst_slice(size_t didx, int ordinal, const HostBurst &hb,
+    uint64_t lo, uint64_t hi)
+{
+	const NumaPlace &np = numa_place(ordinal);
+	NumaBind bind(np);
+	DeviceCtx *c = ctx_for(didx);
+	BurstCtx *b = bctx_for(didx);
+	std::lock_guard<std::mutex> g(b->mu);
+	HIP_TRY(hipSetDevice(ordinal));
+	BurstPins pins;
+	pins.result = is_pinned(hb.result);
+	if (!hb.tx) {
+		pins.iv = hb.iv != nullptr && is_pinned(hb.iv);
+		pins.seq = hb.seq_out != nullptr && is_pinned(hb.seq_out);
+		pins.flags = hb.flags_out != nullptr && is_pinned(hb.flags_out);
+	}
+	const PackPlan all = pack_sizes(*c->pool, hb.lens + lo, hi - lo);
+	const size_t mean = std::max<size_t>(all.start[all.nt] /
+	    std::max<uint64_t>(hi - lo, 1), 16);
+	const uint64_t per_chunk = std::max<size_t>(kChunkBytes / mean, 1);
+	int rc = 0, cur = 0;
+	for (uint64_t at = lo; at < hi && rc == 0;) {
+		const uint64_t end = std::min<uint64_t>(hi, at + per_chunk);
+		BurstSlot &s = b->slot[cur];
+		if ((rc = s.drain()) != 0)
+			break;
+		rc = enqueue_burst_chunk(*c->pool, s, hb, pins, at, end);
+		at = end;
+		cur ^= 1;
+	}
+	/* both slots drained whatever happened: no kernel may still write
+	 * into the caller's memory when the call returns */
+	const int rc2 = b->slot[0].drain();
+	const int rc3 = b->slot[1].drain();
+	return rc ? rc : rc2 ? rc2 : rc3;
+}
+
+/* Host-memory arguments: no device, workspace or size requirement. */
+int check_host_burst(int hash_alg, const void *key, size_t keylen,
+    uint32_t ivlen, const void *base, const uint64_t *offsets,
+    const uint32_t *lens, uint64_t n, const uint8_t *result)
+{
+	if (hash_alg != NET2_HASH_NIL && (hash_alg < NET2_HASH_HMAC_SHA256 ||
+	    hash_alg > NET2_HASH_HMAC_SHA512))
+		return EINVAL;
+	if (hash_alg != NET2_HASH_NIL && ((size_t)kRows[hash_alg].keylen !=
+	    keylen || key == nullptr))
+		return EINVAL;
+	if (ivlen > 64)
+		return EINVAL;
+	if (n == 0)
+		return 0;
+	if (base == nullptr || offsets == nullptr || lens == nullptr ||
+	    result == nullptr || n > UINT32_MAX)
+		return EINVAL;
+	return 0;
+}
+
+}	/* namespace */
+
+NET2_EXPORT int net2_packet_decode_burst_host(
+    const struct net2_burst_rx_keys *k, uint32_t ivlen, const void *base,
+    const uint64_t *offsets, const uint32_t *lens, uint64_t n,
+    uint8_t *result, void *iv, uint32_t *seq, uint32_t *flags,
+    int max_devices)
+{
+	if (k == nullptr)
+		return EINVAL;
+	int rc = check_host_burst(k->hash_alg, k->hash_key, k->hash_keylen,
+	    ivlen, base, offsets, lens, n, result);
+	if (rc != 0 || n == 0)
+		return rc;
+	if (k->hash_alg != NET2_HASH_NIL && k->alt_hash_key != nullptr &&
+	    k->alt_hash_keylen != k->hash_keylen)
+		return EINVAL;
+	if ((seq == nullptr) != (flags == nullptr))
+		return EINVAL;
+	HostBurst hb = {};
+	hb.tx = false;
+	hb.keys = k;
+	hb.ivlen = ivlen;
+	hb.iv = iv;
+	hb.seq_out = seq;
+	hb.flags_out = flags;
+	hb.base = (uint8_t *)const_cast<void *>(base);
+	hb.offsets = offsets;
+	hb.lens = lens;
+	hb.result = result;
+	return shard_batch(n, lens, 0, max_devices, [&](size_t didx,
+	    int ordinal, uint64_t lo, uint64_t hi) {
+		return run_burst_slice(didx, ordinal, hb, lo, hi);
+	});
+}
+
+NET2_EXPORT int net2_packet_encode_burst_host(int hash_alg,
+    const void *hash_key, size_t hash_keylen, int enc_alg,
+    const uint32_t *seq, const uint32_t *flags, void *base,
+    const uint64_t *offsets, const uint32_t *lens, uint64_t n,
+    uint8_t *result, int max_devices)
+{
+	int rc = check_host_burst(hash_alg, hash_key, hash_keylen, 0, base,
+	    offsets, lens, n, result);
+	if (rc != 0 || n == 0)
+		return rc;
+	if (seq == nullptr || flags == nullptr)
+		return EINVAL;
+	HostBurst hb = {};
+	hb.tx = true;
+	hb.hash_alg = hash_alg;
+	hb.hash_key = hash_key;
+	hb.hash_keylen = hash_keylen;
+	hb.enc_alg = enc_alg;
+	hb.seq_in = seq;
+	hb.flags_in = flags;
+	hb.base = (uint8_t *)base;
+	hb.offsets = offsets;
+	hb.lens = lens;
+	hb.result = result;
+	return shard_batch(n, lens, 0, max_devices, [&](size_t didx,
+	    int ordinal, uint64_t lo, uint64_t hi) {
+		return run_burst_slice(didx, ordinal, hb, lo, hi);
+	});
+}

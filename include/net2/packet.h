@@ -55,7 +55,13 @@ int net2_ph_to_iv_dev(const uint32_t *d_seq, const uint32_t *d_flags,
 #define NET2_PENCODE_BAD	2
 #define NET2_PENCODE_UNSAFE	3
 
-/* Device scratch (bytes, 16-byte aligned) of a burst of n datagrams. */
+/*
+ * Device scratch (bytes, 16-byte aligned) of a burst of n datagrams.  Its
+ * length-binning area comes first, at the same place for every n: one
+ * workspace serves bursts of any size up to its own, and
+ * net2_sha2_workspace_init / net2_sha2_workspace_stats (net2/sha2_batch.h)
+ * prepare and inspect it.
+ */
 size_t net2_packet_burst_workspace(uint64_t n);
 
 /*
@@ -137,6 +143,40 @@ int net2_packet_encode_burst(int hash_alg, const void *hash_key,
     const uint32_t *d_flags, void *d_base, const uint64_t *d_offsets,
     const uint32_t *d_lens, uint64_t n, uint8_t *d_result, void *d_ws,
     size_t ws_bytes, void *stream);
+
+/*
+ * Host-memory bursts: the same hash steps for datagrams that live in host
+ * memory -- the reference's case: each received one is a net2_buffer filled
+ * by net2_sockdgram_recv (src/sockdgram.c:67-108) and decoded at
+ * src/connection.c:199; each sent one is built by gather()
+ * (src/connection.c:336-339, :467).  Synchronous; every pointer is host
+ * memory (page-locked or pageable, any mix).  The datagrams are packed into
+ * pinned staging in 64 MiB chunks (two per device in flight: pack, H2D,
+ * kernels, results), sharded over every usable GPU (max_devices <= 0: all;
+ * no slice under 16 MiB; the list starts at the calling thread's current
+ * device, as net2_sha2_batch), each slice's thread on its GPU's NUMA node.
+ * The kernels store results straight into page-locked result arrays and
+ * through pinned staging into pageable ones.
+ *
+ * RX: datagram i = base[offsets[i] .. + lens[i]); result[i] its
+ * NET2_PDECODE_* code, iv + i * ivlen its IV when OK and encrypted (iv may
+ * be NULL), seq[i] / flags[i] the decoded header (both or neither) --
+ * exactly net2_packet_decode_burst_ck's outputs.
+ *
+ * TX: slot i as for net2_packet_encode_burst, in the caller's buffer: for
+ * every slot whose code is NET2_PENCODE_OK the header and (PH_SIGNED) the
+ * HMAC field are written into it; the payload bytes are only read.
+ *
+ * 0, EINVAL, ENOMEM, ENODEV or EIO (then some results may be unset).
+ */
+int net2_packet_decode_burst_host(const struct net2_burst_rx_keys *keys,
+    uint32_t ivlen, const void *base, const uint64_t *offsets,
+    const uint32_t *lens, uint64_t n, uint8_t *result, void *iv,
+    uint32_t *seq, uint32_t *flags, int max_devices);
+int net2_packet_encode_burst_host(int hash_alg, const void *hash_key,
+    size_t hash_keylen, int enc_alg, const uint32_t *seq,
+    const uint32_t *flags, void *base, const uint64_t *offsets,
+    const uint32_t *lens, uint64_t n, uint8_t *result, int max_devices);
 
 #ifdef __cplusplus
 }

@@ -109,16 +109,62 @@ size_t net2_sha2_dev_var_workspace(uint64_t n);
 
 /*
  * Prepare a variable-layout workspace (net2_sha2_dev_var, the variable
- * layouts of net2_hmac_dev / _sign_dev / _verify_dev), asynchronously on
- * `stream`.  Optional: the binning keeps its state in the workspace and
- * cleans up after itself, so a workspace reused call after call needs this
- * at most once; an unprepared one (fresh memory) hashes its first batch in
- * submission order -- same digests, only without the length binning --
- * while it prepares itself.  A workspace must not serve two launches that
- * may run at once.  0, EINVAL (NULL, misaligned or smaller than
- * net2_sha2_dev_var_workspace(0)), ENODEV or EIO.
+ * layouts of net2_hmac_dev / _sign_dev / _verify_dev, and a packet-burst
+ * workspace, net2/packet.h, whose binning area comes first), asynchronously
+ * on `stream`; zeroes its counters (net2_sha2_workspace_stats).  Optional:
+ * the binning keeps its state in the workspace and cleans up after itself,
+ * so a workspace reused call after call needs this at most once; an
+ * unprepared one (fresh memory) hashes its first batch in submission order
+ * -- same digests, only without the length binning -- while it prepares
+ * itself.  A workspace used for other data in between should be prepared
+ * again: the binning detects a histogram that is not its own (the batch is
+ * then hashed in submission order and counted as a mismatch), but only
+ * preparation restores binning from the next call on.  A workspace must not
+ * serve two launches that may run at once.  0, EINVAL (NULL, misaligned or
+ * smaller than net2_sha2_dev_var_workspace(0)), ENODEV or EIO.
  */
 int net2_sha2_workspace_init(void *d_ws, size_t ws_bytes, void *stream);
+
+/*
+ * What the length binning of a workspace has done since
+ * net2_sha2_workspace_init, or since the first use of a fresh one
+ * (diagnostics; the binning falls back to submission order -- same digests,
+ * slower -- and counts why):
+ *   prepared    the header is valid (the next launch bins);
+ *   binned      launches whose grid barrier completed (binned, unless
+ *               counted as a mismatch too);
+ *   aborts      grid barriers that timed out (the binning grid was not
+ *               co-resident, e.g. beside long kernels on other streams);
+ *   mismatches  launches whose global histogram did not add up to the
+ *               batch (the workspace was overwritten between calls);
+ *   unprepared  launches that found the header unprepared (fresh memory, or
+ *               the launch after an abort or a mismatch).
+ */
+struct net2_bin_stats {
+	uint32_t prepared;
+	uint32_t binned;
+	uint32_t aborts;
+	uint32_t mismatches;
+	uint32_t unprepared;
+};
+
+/*
+ * Reads a workspace's counters (synchronous device-to-host copy of its
+ * header; synchronise the streams that use it first).  0, EINVAL, ENODEV
+ * or EIO.
+ */
+int net2_sha2_workspace_stats(const void *d_ws, size_t ws_bytes,
+    struct net2_bin_stats *stats);
+
+/*
+ * Limits of the one-launch binning, process-wide (diagnostics and tests):
+ * grid_cap caps its persistent grid (0: the device's co-resident capacity
+ * of the binning kernel, at most 256 workgroups -- the default); timeout_us
+ * is how long its grid barrier waits for every workgroup before deciding
+ * ABORT (< 0: the default 50 ms; 0 makes every launch whose workgroups are
+ * not all there at once abort).  Always 0.
+ */
+int net2_sha2_bin_limits(uint32_t grid_cap, int64_t timeout_us);
 
 /*
  * Host-memory batch, end to end: packets are read from host memory (DMA'd

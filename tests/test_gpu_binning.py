@@ -1,13 +1,12 @@
-"""The one-pass length binning (bin_onepass_kernel):
-one launch counts, scans and scatters, keeping its state in the caller's
-workspace and cleaning up after itself.  Checked through the C ABI: every
-digest against the oracle, and the visiting order itself (the perm words of
-the workspace) -- a permutation of the batch, longest block count first
-when binned, submission order when the workspace was not prepared or the
-grid barrier was decided ABORT."""
+"""The one-pass length binning (bin_onepass_kernel): one launch counts, scans
+and scatters, keeping its state in the caller's workspace and cleaning up
+after itself.  Checked through the C ABI: every digest against the oracle,
+the visiting order itself (the perm words of the workspace) -- a permutation
+of the batch, longest block count first when binned, submission order when
+the workspace was not prepared or the grid barrier was decided ABORT -- and
+the workspace's counters (net2_sha2_workspace_stats): a fallback to
+submission order is never silent."""
 import os
-import subprocess
-import sys
 
 import numpy as np
 import pytest
@@ -156,46 +155,246 @@ def test_many_tiles_per_workgroup(dev, oracle_mod):
     assert (np.diff(_blocks(lens, 3)[order]) <= 0).all()
 
 
-_ABORT = r'''
-import sys
-sys.path.insert(0, "."); sys.path.insert(0, "tests")
-import numpy as np, torch
-import synth
-from oracle import oracle
-from ilias_net2_amd import batch, _lib
-L = _lib.lib()
-dev = torch.device("cuda:0")
-n = 200_000
-lens = synth.mixed_lengths(640, n)
-data, offs = synth.packed(641, lens)
-want = oracle.batch(1, data, offsets=offs, lens=lens, nthreads=16)
-d = torch.from_numpy(data).to(dev)
-o = torch.from_numpy(offs.astype(np.int64)).to(dev)
-ln = torch.from_numpy(lens.astype(np.int32)).to(dev)
-ws = batch.var_workspace(n, dev)
-bad = 0
-for _ in range(12):
-    got = batch.digest_var(1, d, o, ln, workspace=ws)
+def _stats(L, ws):
+    from ilias_net2_amd import _lib
     torch.cuda.synchronize()
-    bad += not np.array_equal(got.cpu().numpy(), want)
-    order = ws.cpu().numpy()[L.net2_sha2_dev_var_workspace(0) // 4:][:n]
-    bad += not np.array_equal(np.sort(order), np.arange(n))
-hm = batch.hmac_dev(6, bytes(64), d, offsets=o, lens=ln, workspace=ws)
-torch.cuda.synchronize()
-bad += not np.array_equal(hm.cpu().numpy()[::997], np.stack([
-    np.frombuffer(oracle.hmac(6, bytes(64), data[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes()),
-                  dtype=np.uint8) for i in range(0, n, 997)]))
-print("BAD", bad)
-'''
+    return _lib.workspace_stats(ws.data_ptr(), ws.numel() * ws.element_size())
 
 
-def test_barrier_timeout_takes_submission_order():
-    """NET2_BIN_TIMEOUT_US=0: the grid barrier may be decided ABORT before
-    every workgroup arrives -- then all of them take the submission order
-    and the header re-initialises at the next call.  Whatever each call
-    decides, its digests and order are right (fresh process)."""
-    env = dict(os.environ, NET2_BIN_TIMEOUT_US="0")
-    r = subprocess.run([sys.executable, "-c", _ABORT], cwd=ROOT, env=env,
-                       capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout + r.stderr
-    assert "BAD 0" in r.stdout, r.stdout + r.stderr
+@pytest.fixture
+def bin_limits():
+    """net2_sha2_bin_limits for one test, the defaults restored after."""
+    from ilias_net2_amd import _lib
+    L = _lib.lib()
+    yield lambda cap, timeout_us: L.net2_sha2_bin_limits(cap, timeout_us)
+    L.net2_sha2_bin_limits(0, -1)
+
+
+def _c3(n, seed, alg=1):
+    lens = synth.mixed_lengths(seed, n)
+    data, offs = synth.packed(seed + 1, lens)
+    return lens, data, offs
+
+
+def _dev_args(dev, data, offs, lens):
+    return (torch.from_numpy(data).to(dev),
+            torch.from_numpy(offs.astype(np.int64)).to(dev),
+            torch.from_numpy(lens.astype(np.int32)).to(dev))
+
+
+def test_barrier_timeout_takes_submission_order(dev, oracle_mod, bin_limits):
+    """A zero barrier timeout: a launch whose workgroups are not all there
+    when the first one polls is decided ABORT -- all of them take the
+    submission order and the header re-initialises at the next call.
+    Whatever each call decides, its digests and order are right, and every
+    launch is accounted for: unprepared + aborted + binned."""
+    from ilias_net2_amd import _lib, batch
+    L = _lib.lib()
+    bin_limits(0, 0)
+    n = 200_000
+    lens, data, offs = _c3(n, 640)
+    want = oracle_mod.batch(1, data, offsets=offs, lens=lens, nthreads=16)
+    d, o, ln = _dev_args(dev, data, offs, lens)
+    ws = batch.var_workspace(n, dev)
+    calls = 12
+    for _ in range(calls):
+        got = batch.digest_var(1, d, o, ln, workspace=ws)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy(), want)
+        assert np.array_equal(np.sort(_order(ws, L, n)), np.arange(n))
+    hm = batch.hmac_dev(6, bytes(64), d, offsets=o, lens=ln, workspace=ws)
+    torch.cuda.synchronize()
+    idx = range(0, n, 997)
+    assert np.array_equal(hm.cpu().numpy()[::997], np.stack([
+        np.frombuffer(oracle_mod.hmac(6, bytes(64), data[int(offs[i]):int(offs[i]) +
+                      int(lens[i])].tobytes()), dtype=np.uint8) for i in idx]))
+    st = _stats(L, ws)
+    assert st["mismatches"] == 0
+    assert st["unprepared"] + st["aborts"] + st["binned"] == calls + 1, st
+    assert st["aborts"] > 0, st
+
+
+def test_fresh_workspace_does_not_abort(dev, oracle_mod):
+    """A fresh (zeroed) workspace under a full 256-workgroup grid: the first
+    launch takes the submission order while workgroup 0 prepares the header;
+    a workgroup dispatched after that must not mistake the header for a
+    prepared one (it carries this launch's id) and join a barrier the early
+    workgroups skipped -- no 50 ms stall, no abort.  The next launches bin."""
+    from ilias_net2_amd import _lib, batch
+    L = _lib.lib()
+    n = 1 << 20
+    lens, data, offs = _c3(n, 660)
+    want = oracle_mod.batch(1, data, offsets=offs, lens=lens, nthreads=16)
+    d, o, ln = _dev_args(dev, data, offs, lens)
+    for rep in range(3):
+        ws = torch.zeros(L.net2_sha2_dev_var_workspace(n) // 4, dtype=torch.int32,
+                         device=dev)
+        for call in range(3):
+            got = batch.digest_var(1, d, o, ln, workspace=ws)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy(), want), (rep, call)
+        st = _stats(L, ws)
+        assert st == {"prepared": 1, "binned": 2, "aborts": 0, "mismatches": 0,
+                      "unprepared": 1}, (rep, st)
+        assert (np.diff(_blocks(lens, 1)[_order(ws, L, n)]) <= 0).all()
+
+
+@pytest.mark.parametrize("cap", [1, 3, 40])
+def test_grid_capped_below_the_tiles(dev, oracle_mod, bin_limits, cap):
+    """The persistent grid capped (as on a partitioned device, or by
+    net2_sha2_bin_limits): each workgroup bins many tiles, the barrier still
+    completes, the order is binned."""
+    from ilias_net2_amd import _lib, batch
+    L = _lib.lib()
+    bin_limits(cap, -1)
+    n = 300_000
+    lens, data, offs = _c3(n, 670)
+    want = oracle_mod.batch(3, data, offsets=offs, lens=lens, nthreads=16)
+    d, o, ln = _dev_args(dev, data, offs, lens)
+    ws = batch.var_workspace(n, dev)
+    for _ in range(2):
+        got = batch.digest_var(3, d, o, ln, workspace=ws)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy(), want)
+        order = _order(ws, L, n)
+        assert np.array_equal(np.sort(order), np.arange(n))
+        assert (np.diff(_blocks(lens, 3)[order]) <= 0).all()
+    st = _stats(L, ws)
+    assert st["binned"] == 2 and st["aborts"] == 0 and st["mismatches"] == 0, st
+
+
+@pytest.mark.parametrize("nstreams", [2, 4])
+def test_concurrent_streams_bin_without_aborts(dev, oracle_mod, nstreams):
+    """C3 batches on several streams at once, each with its own workspace
+    (DESIGN 5.6's two-stream overlap, and four): the binning grids run next
+    to each other's hash kernels; every launch must still bin -- no barrier
+    abort, block counts non-increasing along each order -- and every digest
+    be right."""
+    from ilias_net2_amd import _lib, batch
+    L = _lib.lib()
+    n = (1 << 20) // nstreams
+    jobs = []
+    for k in range(nstreams):
+        lens, data, offs = _c3(n, 700 + k)
+        want = oracle_mod.batch(1, data, offsets=offs, lens=lens, nthreads=16)
+        d, o, ln = _dev_args(dev, data, offs, lens)
+        jobs.append(dict(lens=lens, want=want, d=d, o=o, ln=ln,
+                         ws=batch.var_workspace(n, dev),
+                         out=torch.empty((n, 32), dtype=torch.uint8, device=dev),
+                         s=torch.cuda.Stream(dev)))
+    torch.cuda.synchronize()
+    rounds = 8
+    for _ in range(rounds):
+        for j in jobs:
+            with torch.cuda.stream(j["s"]):
+                batch.digest_var(1, j["d"], j["o"], j["ln"], out=j["out"],
+                                 workspace=j["ws"], stream=j["s"])
+    torch.cuda.synchronize()
+    for j in jobs:
+        assert np.array_equal(j["out"].cpu().numpy(), j["want"])
+        order = _order(j["ws"], L, n)
+        assert np.array_equal(np.sort(order), np.arange(n))
+        assert (np.diff(_blocks(j["lens"], 1)[order]) <= 0).all()
+        st = _stats(L, j["ws"])
+        assert st == {"prepared": 1, "binned": rounds, "aborts": 0,
+                      "mismatches": 0, "unprepared": 0}, st
+
+
+def test_overwritten_workspace_is_detected(dev, oracle_mod):
+    """A caller reuses the workspace for other data between calls (here:
+    stale counts in the next launch's histogram, then barrier counters that
+    fire the grid barrier early): the binning finds that its histogram does
+    not add up to the batch and the hash kernel falls back to submission
+    order -- digests right, the mismatch counted, binning back two calls
+    later."""
+    from ilias_net2_amd import _lib, batch
+    L = _lib.lib()
+    n = 400_000
+    lens, data, offs = _c3(n, 680)
+    want = oracle_mod.batch(1, data, offsets=offs, lens=lens, nthreads=16)
+    d, o, ln = _dev_args(dev, data, offs, lens)
+    ws = batch.var_workspace(n, dev)
+    hdr, nb = 16, 2048
+    ctl0 = hdr + 2 * nb
+    G = (n + 4095) // 4096
+
+    def run():
+        got = batch.digest_var(1, d, o, ln, workspace=ws)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy(), want)
+
+    def epoch():
+        torch.cuda.synchronize()
+        return int(ws[2].item())
+
+    run()
+    assert epoch() == 1 and _stats(L, ws)["binned"] == 1
+    par = epoch() & 1
+    # 1. stale counts in the next parity's histogram
+    ws[hdr + par * nb + 7] += 5
+    run()
+    st = _stats(L, ws)
+    assert st["mismatches"] == 1 and not st["prepared"], st
+    run()                                   # re-initialises: submission order
+    run()                                   # binned again
+    st = _stats(L, ws)
+    assert st["prepared"] and st["unprepared"] == 1 and st["binned"] == 3, st
+    assert (np.diff(_blocks(lens, 1)[_order(ws, L, n)]) <= 0).all()
+    # 2. barrier words that decide GO at the first arrival: whatever the
+    # workgroups then read, the digests stay right
+    for _ in range(3):
+        base = ctl0 + (epoch() & 1) * 1024
+        ws[base + 512] = min(G, 16) - 1     # top counter: one arrival short
+        ws[base + 0] = (G + 15) // 16 - 1   # group 0: its first arrival is last
+        run()
+        run()
+    st = _stats(L, ws)
+    assert st["aborts"] == 0, st
+
+
+def test_burst_workspace_reused_across_sizes(dev, oracle_mod):
+    """One packet-burst workspace sized for the largest burst serves bursts
+    of other sizes in turn (its binning area sits at offset 0 whatever n is,
+    so another burst's status and verdict bytes can no longer land on the
+    histogram); each burst mixes sealed and forged datagrams, every code
+    against the oracle."""
+    from ilias_net2_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(90)
+    nmax, alg, ivlen = 200_000, 6, 16
+    key = bytes(range(64))
+    ws = torch.empty(L.net2_packet_burst_workspace(nmax), dtype=torch.uint8,
+                     device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    for m in (nmax, 70_001, 150_000, 4096, nmax, 333, 199_999):
+        lens = rng.choice(np.array([136, 584, 1500], dtype=np.uint32), m)
+        offs = np.zeros(m, dtype=np.uint64)
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        data = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+        seq = rng.integers(0, 2**32, m, dtype=np.uint64).astype(np.uint32)
+        flags = np.full(m, 3, dtype=np.uint32)
+        r, sealed = oracle_mod.packet_encode_batch(alg, key, True, seq, flags, data,
+                                                   offs, lens, nthreads=16)
+        forged = rng.random(m) < 0.2       # sealed with the wrong key
+        r2, sealed2 = oracle_mod.packet_encode_batch(alg, bytes(64), True, seq, flags,
+                                                     data, offs, lens, nthreads=16)
+        for i in np.nonzero(forged)[0]:
+            a = int(offs[i])
+            sealed[a:a + 72] = sealed2[a:a + 72]
+        want = oracle_mod.packet_decode_batch(alg, key, True, ivlen, sealed, offs,
+                                              lens, nthreads=16)
+        assert np.array_equal(want[0] != 0, forged)
+        d = torch.from_numpy(sealed).to(dev)
+        o = torch.from_numpy(offs.view(np.int64)).to(dev)
+        ln = torch.from_numpy(lens.view(np.int32)).to(dev)
+        res = torch.full((m,), 9, dtype=torch.uint8, device=dev)
+        iv = torch.zeros((m, ivlen), dtype=torch.uint8, device=dev)
+        assert L.net2_packet_decode_burst(alg, key, 64, 1, ivlen, d.data_ptr(),
+                                          o.data_ptr(), ln.data_ptr(), m,
+                                          res.data_ptr(), iv.data_ptr(), None, None,
+                                          ws.data_ptr(), ws.numel(), st) == 0
+        assert np.array_equal(res.cpu().numpy(), want[0]), m
+        ok = want[0] == 0
+        assert np.array_equal(iv.cpu().numpy()[ok], want[1][ok]), m
+    s = _lib.workspace_stats(ws.data_ptr(), ws.numel())
+    assert s["aborts"] == 0 and s["mismatches"] == 0, s
