@@ -180,6 +180,8 @@ def lib() -> ctypes.CDLL:
         _share_torch_hip_runtime()
         handle = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if "NET2_SHA2_LIB" in os.environ and not hasattr(handle, name):
+                continue    # an A/B build of an earlier round: older ABI
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args

@@ -54,6 +54,145 @@ iov_len(const struct iovec *iov, size_t n)
 #define NET2_SC_FEW 16			/* the coalescer's wave-form batch */
 #define NET2_SC_LONG_BYTES 8192		/* mean payload above which it pays */
 
+/*
+ * Helper threads of the tick, started once and kept: the hash requests of a
+ * few long payloads (hash_few_long) and the work after the hash (run_jobs)
+ * run on them instead of on threads created and joined every tick.  A
+ * batch's tasks go on one queue that every worker -- and the submitting
+ * thread, while it waits for its batch -- takes from, so concurrent ticks
+ * share the workers and none waits on a task nobody runs.  The workers are
+ * detached and live as long as the process.
+ */
+#define NET2_SC_MAXTHREADS 64
+
+struct sc_batch {
+	size_t		left;		/* tasks not finished */
+	pthread_cond_t	done;
+};
+
+struct sc_task {
+	void		*(*fn)(void *);
+	void		*arg;
+	struct sc_batch	*b;
+};
+
+static struct {
+	pthread_mutex_t	mu;
+	pthread_cond_t	work;
+	struct sc_task	*q;		/* ring of qcap tasks */
+	size_t		qcap, qhead, qlen;
+	int		nworkers;
+} g_pool = { PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, NULL,
+    0, 0, 0, 0 };
+
+/* the next queued task, under g_pool.mu; 0 if none */
+static int
+pool_pop(struct sc_task *t)
+{
+	if (g_pool.qlen == 0)
+		return 0;
+	*t = g_pool.q[g_pool.qhead];
+	g_pool.qhead = (g_pool.qhead + 1) % g_pool.qcap;
+	g_pool.qlen--;
+	return 1;
+}
+
+/* run t outside the lock, then count it done (lock held on entry/exit) */
+static void
+pool_run(struct sc_task *t)
+{
+	pthread_mutex_unlock(&g_pool.mu);
+	t->fn(t->arg);
+	pthread_mutex_lock(&g_pool.mu);
+	if (--t->b->left == 0)
+		pthread_cond_broadcast(&t->b->done);
+}
+
+static void *
+pool_worker(void *unused)
+{
+	struct sc_task t;
+
+	(void)unused;
+	pthread_mutex_lock(&g_pool.mu);
+	for (;;) {
+		while (!pool_pop(&t))
+			pthread_cond_wait(&g_pool.work, &g_pool.mu);
+		pool_run(&t);
+	}
+	return NULL;
+}
+
+/*
+ * fn(args[k]) for k < n, on the calling thread and up to nthreads - 1
+ * helpers; returns when all are done.  Tasks that cannot be queued (no
+ * memory) or find no helper run on the calling thread.
+ */
+static void
+pool_run_batch(void *(*fn)(void *), void **args, size_t n, int nthreads)
+{
+	struct sc_batch b;
+	struct sc_task t;
+	size_t k;
+
+	if (n == 0)
+		return;
+	if (n == 1 || nthreads <= 1) {
+		for (k = 0; k < n; k++)
+			fn(args[k]);
+		return;
+	}
+	b.left = n - 1;
+	pthread_cond_init(&b.done, NULL);
+	pthread_mutex_lock(&g_pool.mu);
+	/* room for this batch's tasks on the ring */
+	if (g_pool.qcap < g_pool.qlen + n) {
+		size_t cap = 2 * (g_pool.qlen + n);
+		struct sc_task *q = malloc(cap * sizeof(*q));
+		if (q != NULL) {
+			for (k = 0; k < g_pool.qlen; k++)
+				q[k] = g_pool.q[(g_pool.qhead + k) % g_pool.qcap];
+			free(g_pool.q);
+			g_pool.q = q;
+			g_pool.qcap = cap;
+			g_pool.qhead = 0;
+		}
+	}
+	if (g_pool.qcap < g_pool.qlen + n) {
+		pthread_mutex_unlock(&g_pool.mu);
+		pthread_cond_destroy(&b.done);
+		for (k = 0; k < n; k++)
+			fn(args[k]);
+		return;
+	}
+	while (g_pool.nworkers < nthreads - 1 &&
+	    g_pool.nworkers < NET2_SC_MAXTHREADS - 1) {
+		pthread_t tid;
+		if (pthread_create(&tid, NULL, pool_worker, NULL) != 0)
+			break;
+		pthread_detach(tid);
+		g_pool.nworkers++;
+	}
+	for (k = 1; k < n; k++) {
+		g_pool.q[(g_pool.qhead + g_pool.qlen) % g_pool.qcap] =
+		    (struct sc_task){ fn, args[k], &b };
+		g_pool.qlen++;
+	}
+	pthread_cond_broadcast(&g_pool.work);
+	pthread_mutex_unlock(&g_pool.mu);
+	fn(args[0]);
+	pthread_mutex_lock(&g_pool.mu);
+	/* help with whatever is queued until this batch is done */
+	while (b.left > 0) {
+		if (pool_pop(&t))
+			pool_run(&t);
+		else
+			pthread_cond_wait(&b.done, &g_pool.mu);
+	}
+	pthread_mutex_unlock(&g_pool.mu);
+	pthread_cond_destroy(&b.done);
+}
+
 struct one_hash {
 	const struct payload_ref *p;
 	int alg, rc;
@@ -73,24 +212,18 @@ static int
 hash_few_long(struct payload_ref *p, size_t np, int alg)
 {
 	struct one_hash job[NET2_SC_FEW];
-	pthread_t tid[NET2_SC_FEW];
-	int started[NET2_SC_FEW];
+	void *args[NET2_SC_FEW];
 	size_t m = 0;
 	int rc = 0;
 
 	for (size_t i = 0; i < np; i++)
-		if (p[i].alg == alg)
-			job[m++] = (struct one_hash){ &p[i], alg, 0 };
-	for (size_t k = 1; k < m; k++)
-		started[k] = pthread_create(&tid[k], NULL, one_hash_run,
-		    &job[k]) == 0;
-	one_hash_run(&job[0]);
-	for (size_t k = 1; k < m; k++) {
-		if (started[k])
-			pthread_join(tid[k], NULL);
-		else
-			one_hash_run(&job[k]);	/* could not start a thread */
-	}
+		if (p[i].alg == alg) {
+			job[m] = (struct one_hash){ &p[i], alg, 0 };
+			args[m] = &job[m];
+			m++;
+		}
+	/* all at once, so the coalescer batches them */
+	pool_run_batch(one_hash_run, args, m, (int)m);
 	for (size_t k = 0; k < m; k++)
 		if (job[k].rc != 0) {
 			if (*job[k].p->rc == 0)
@@ -277,32 +410,25 @@ ecdsa_run(void *arg)
 static void
 run_jobs(const struct ecdsa_plan *pl, int nthreads)
 {
-	struct ecdsa_slice sl[64];
-	pthread_t tid[64];
-	int t, started;
+	struct ecdsa_slice sl[NET2_SC_MAXTHREADS];
+	void *args[NET2_SC_MAXTHREADS];
+	int t;
 
 	if (nthreads <= 0) {
 		long c = sysconf(_SC_NPROCESSORS_ONLN);
 		nthreads = c > 0 ? (int)c : 1;
 	}
-	if (nthreads > 64)
-		nthreads = 64;
+	if (nthreads > NET2_SC_MAXTHREADS)
+		nthreads = NET2_SC_MAXTHREADS;
 	if ((size_t)nthreads > pl->njobs)
 		nthreads = pl->njobs ? (int)pl->njobs : 1;
 	for (t = 0; t < nthreads; t++) {
 		sl[t].pl = pl;
 		sl[t].lo = pl->njobs * t / nthreads;
 		sl[t].hi = pl->njobs * (t + 1) / nthreads;
+		args[t] = &sl[t];
 	}
-	for (started = 1; started < nthreads; started++)
-		if (pthread_create(&tid[started], NULL, ecdsa_run,
-		    &sl[started]) != 0)
-			break;
-	ecdsa_run(&sl[0]);
-	for (t = started; t < nthreads; t++)	/* threads we could not start */
-		ecdsa_run(&sl[t]);
-	for (t = 1; t < started; t++)
-		pthread_join(tid[t], NULL);
+	pool_run_batch(ecdsa_run, args, (size_t)nthreads, nthreads);
 }
 
 /* validate_prologue of signature.c (signature.n2t:133-145): hash row of a
@@ -424,6 +550,14 @@ tick(struct net2_sc_hash_req **hreq, size_t nh,
 	pl.sjob = sjob;
 	pl.nsig_jobs = sjob[ns];
 	pl.njobs = sjob[ns] + nv + nh;
+	/* the hash requests' part of the tick's outcome, taken now: their rc
+	 * is final once hashing is done, and a callback may free or reuse its
+	 * request */
+	int h_all = 1, h_first = 0;
+	for (size_t i = 0; i < nh && h_all; i++) {
+		h_all = hreq[i]->rc != 0;
+		h_first = h_first ? h_first : hreq[i]->rc;
+	}
 	if (pl.njobs > 0)
 		run_jobs(&pl, nthreads);
 	/* a carver whose signing failed keeps none of its signatures */
@@ -438,11 +572,7 @@ tick(struct net2_sc_hash_req **hreq, size_t nh,
 	 * request carries too.  Otherwise 0, and the per-request rc / result
 	 * values are the outcome. */
 	{
-		int all = 1, first = 0;
-		for (size_t i = 0; i < nh && all; i++) {
-			all = hreq[i]->rc != 0;
-			first = first ? first : hreq[i]->rc;
-		}
+		int all = h_all, first = h_first;
 		for (size_t i = 0; i < ns && all; i++) {
 			all = sreq[i].rc != 0;
 			first = first ? first : sreq[i].rc;

@@ -168,7 +168,7 @@ struct Sha512H : Sha512 {
  * while the current one is compressed -- a prefetch that costs no VGPRs
  * (absorb below; spill-free, profiles/round3/hmac512_spillfree_ab*.txt) */
 #ifndef NET2_HF_GLDS
-#define NET2_HF_GLDS 0
+#define NET2_HF_GLDS 1
 #endif
 struct Sha512HF : Sha512 {
 	static constexpr bool GLDS = NET2_HF_GLDS != 0;

@@ -234,8 +234,12 @@ def test_integration_carver_binding_compiles_with_reference_headers(tmp_path):
     C++): no error, so no conflicting declaration -- a C-linkage function
     declared twice with different prototypes is an error in C++."""
     blocks = _integration_snippets()
-    assert len(blocks) >= 2, "INTEGRATION.md lost its compiled blocks"
+    assert len(blocks) >= 3, "INTEGRATION.md lost its compiled blocks"
     assert any("net2_sc_hash_req" in b for b in blocks)
+    # the host-memory datagram path: the receive loop over the reference's
+    # own net2_sockdgram_recv and the TX burst onto net2_sockdgram_send
+    assert any("net2_packet_decode_burst_host" in b and "net2_sockdgram_recv" in b
+               for b in blocks)
     cfg_inc, _ = _instantiate_config(str(tmp_path))
     tu = os.path.join(str(tmp_path), "binding.cc")
     with open(tu, "w") as fh:
@@ -252,7 +256,8 @@ def test_integration_carver_binding_compiles_with_reference_headers(tmp_path):
     # the binding really uses the reference's own sign calls
     body = "\n".join(blocks)
     for name in ("net2_signctx_sign(", "net2_signctx_validate(",
-                 "net2_sc_collector_add_hash(", "net2_sc_collector_tick("):
+                 "net2_sc_collector_add_hash(", "net2_sc_collector_tick(",
+                 "net2_packet_encode_burst_host(", "net2_sockdgram_send("):
         assert name in body, name
 
 
