@@ -550,6 +550,19 @@ def rooflines(name, launch_ms, per_launch, sclk_mhz=None):
             "library is %s: counters not reported" % (
                 name, pmc.get("kernel_build_id"), library_build_id()))
         pmc = None
+    pmc_mhz = (pmc.get("clock_ghz_under_pmc") or 0) * 1e3 if pmc else 0
+    if pmc and sclk_mhz and pmc_mhz and abs(pmc_mhz / sclk_mhz - 1) > 0.03:
+        # counters taken at another shader clock than this line's timed
+        # steps (a throttled or other box): per-launch counts would still
+        # hold, but the cycle figures priced with them would not
+        roof["traffic_note"] = (
+            "profiles/pmc_%s.json was measured at %.0f MHz, this line's timed "
+            "steps at %.0f MHz (> 3 %% apart): counters not joined" % (
+                name, pmc_mhz, sclk_mhz))
+        pmc = None
+    if pmc:
+        roof["counters_clock_mhz"] = round(pmc_mhz) if pmc_mhz else None
+        roof["counters_box"] = pmc.get("trace_box")
     if pmc:
         roof["traffic"] = pmc.get("hbm_bytes_per_launch")
         roof["traffic_build_id"] = pmc.get("kernel_build_id")
@@ -559,7 +572,10 @@ def rooflines(name, launch_ms, per_launch, sclk_mhz=None):
     if pmc and pmc.get("valu_wave_instr_per_launch"):
         instr = pmc["valu_wave_instr_per_launch"]
         rate = instr / (launch_ms / 1e3)
-        clk = pmc.get("clock_ghz_under_pmc") or 2.4
+        # cycles at this line's own clock (the counted instructions do not
+        # depend on it; the launch time does)
+        clk = (sclk_mhz / 1e3 if sclk_mhz else None) or \
+            pmc.get("clock_ghz_under_pmc") or 2.4
         valu = {"bound": "valu", "achieved": round(rate / 1e12, 4),
                 "peak": round(VALU_PEAK_WAVE_INSTR / 1e12, 4),
                 "unit": "T wave64-VALU-instr/s",

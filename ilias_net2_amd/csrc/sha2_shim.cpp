@@ -1672,10 +1672,16 @@ struct BurstSlot {
 		if (!busy)
 			return 0;
 		busy = false;
+		const double t0 = dbg_now();
 		HIP_TRY(hipEventSynchronize(done));
+		const double t1 = dbg_now();
 		std::function<int()> f;
 		f.swap(finish);
-		return f ? f() : 0;
+		const int rc = f ? f() : 0;
+		if (dbg_timing())
+			fprintf(stderr, "net2 burst: wait %.3f ms, finish %.3f ms\n",
+			    t1 - t0, dbg_now() - t1);
+		return rc;
 	}
 };
 
@@ -1756,8 +1762,12 @@ int enqueue_burst_chunk(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 	int rc;
 	if ((rc = s.reserve(bytes, n)) != 0)
 		return rc;
+	const double tp0 = dbg_now();
 	pack_fill(pool, plan, s.h_in, s.h_off, s.h_len, hb.base, hb.offsets + lo,
 	    hb.lens + lo, n);
+	if (dbg_timing())
+		fprintf(stderr, "net2 burst: pack %zu B: %.3f ms (%zu threads)\n",
+		    bytes, dbg_now() - tp0, plan.nt);
 	if (bytes != 0)
 		HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
 		    hipMemcpyHostToDevice, s.stream));
@@ -1885,9 +1895,15 @@ int run_burst_slice(size_t didx, int ordinal, const HostBurst &hb,
 	for (uint64_t at = lo; at < hi && rc == 0;) {
 		const uint64_t end = std::min<uint64_t>(hi, at + per_chunk);
 		BurstSlot &s = b->slot[cur];
+		const double t0 = dbg_now();
 		if ((rc = s.drain()) != 0)
 			break;
+		const double t1 = dbg_now();
 		rc = enqueue_burst_chunk(*c->pool, s, hb, pins, at, end);
+		if (dbg_timing())
+			fprintf(stderr, "net2 burst: drain+finish %.3f ms, enqueue "
+			    "%.3f ms (%llu datagrams)\n", t1 - t0, dbg_now() - t1,
+			    (unsigned long long)(end - at));
 		at = end;
 		cur ^= 1;
 	}

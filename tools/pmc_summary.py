@@ -87,6 +87,23 @@ def main():
     res = {"config": args.cfg, "kernel": pat + MODE.get(args.cfg, ""), "dispatches_per_pass": len(durs_all) and
            max(len(v) for v in counters.values()),
            "counters_median_per_launch": med}
+    # the box and clock the trace pass ran at: its bench.py line (the trace
+    # average is only comparable with a bench line of the same clock)
+    log = os.path.join(args.src, f"prof_{args.cfg}.log")
+    if os.path.exists(log):
+        line = None
+        with open(log) as f:
+            for ln in f:
+                if ln.startswith("{"):
+                    line = ln
+        if line:
+            b = json.loads(line)
+            g = b.get("gpu", {})
+            res["trace_box"] = {"host": g.get("host"), "pci": g.get("pci"),
+                                "sclk_mhz_during_timed_steps":
+                                    g.get("sclk_mhz_during_timed_steps"),
+                                "bench_kernel_ms": b.get("roofline", {}).get("kernel_ms"),
+                                "bench_ms_per_step": b.get("ms_per_step")}
     stats_csv = os.path.join(args.src, f"prof_{args.cfg}", "run_kernel_stats.csv")
     if os.path.exists(stats_csv):
         with open(stats_csv) as f:
