@@ -166,12 +166,11 @@ struct Sha512H : Sha512 {
 /* ... and for the fixed-layout HMAC-SHA512 kernel: drain priority kept, the
  * next block fetched with LDS-DMA (global_load_lds) into a per-wave LDS slab
  * while the current one is compressed -- a prefetch that costs no VGPRs
- * (absorb below; spill-free, profiles/round3/hmac512_spillfree_ab*.txt) */
-#ifndef NET2_HF_GLDS
-#define NET2_HF_GLDS 1
-#endif
+ * (absorb below).  96 VGPRs, its ~35 KB of slabs per workgroup hold it at
+ * 4 waves per SIMD; without them it runs 5 waves at 95 VGPRs and measured
+ * 0.7 % slower (profiles/round5/ab_hostmid_box2.txt) */
 struct Sha512HF : Sha512 {
-	static constexpr bool GLDS = NET2_HF_GLDS != 0;
+	static constexpr bool GLDS = true;
 };
 
 /* ---- message loading ------------------------------------------------- */
@@ -1112,9 +1111,11 @@ __device__ __forceinline__ void hmac_item(uint64_t g,
 		len = live ? fixed_len : 0;
 	}
 	uint32_t rx_st = PKT_OK, rx_seq = 0, rx_fl = 0;
-	/* TX with rx.rec: header and hash field to a record of their own
-	 * (field at +0, header at +dlen; the host path) instead of in place;
-	 * its address is formed where it is used (not held across the hash) */
+	/* TX with rx.rec (the host path): instead of sealing in place, every
+	 * live lane fills the record of its binned position g -- hash field at
+	 * +0, then header, datagram index and code -- so a wave's stores cover
+	 * one contiguous stretch of (host) memory; the address is formed where
+	 * it is used, not held across the hash */
 	if (MODE == HMAC_BURST_TX) {
 		if (live) {
 			rx_seq = rx.seq[i];
@@ -1126,25 +1127,26 @@ __device__ __forceinline__ void hmac_item(uint64_t g,
 			rx_st = PKT_UNSAFE;
 		else if (len < 8 + dlen)
 			rx_st = PKT_RESOURCE;	/* no room for header and hash */
-		if (live && rx_st == PKT_OK) {
-			if (rx.rec != nullptr) {
-				*reinterpret_cast<uint2 *>(rx.rec + i * (dlen + 16) +
-				    dlen) = make_uint2(bswap32(rx_seq),
-				    bswap32(rx_fl));
-			} else {
-				uint8_t *h = out + (p - base);
+		const bool ok = live && rx_st == PKT_OK;
+		if (live && rx.rec != nullptr) {
+			*reinterpret_cast<uint4 *>(rx.rec + g * (dlen + 16) + dlen) =
+			    make_uint4(ok ? bswap32(rx_seq) : 0u,
+			    ok ? bswap32(rx_fl) : 0u, (uint32_t)i, rx_st);
+		} else if (ok) {
+			uint8_t *h = out + (p - base);
 #pragma unroll
-				for (int b = 0; b < 4; b++) {
-					h[b] = (uint8_t)(rx_seq >> (24 - 8 * b));
-					h[4 + b] = (uint8_t)(rx_fl >> (24 - 8 * b));
-				}
+			for (int b = 0; b < 4; b++) {
+				h[b] = (uint8_t)(rx_seq >> (24 - 8 * b));
+				h[4 + b] = (uint8_t)(rx_fl >> (24 - 8 * b));
 			}
+		}
+		if (ok) {
 			p += 8;
 			len -= 8;
 		} else {
 			len = 0;
 		}
-		if (live)
+		if (live && rx.rec == nullptr)
 			rx.status[i] = (uint8_t)rx_st;
 	}
 	if (MODE == HMAC_BURST_RX) {
@@ -1251,7 +1253,7 @@ __device__ __forceinline__ void hmac_item(uint64_t g,
 	if (SIGNS && short_dgram)
 		return;
 	if (MODE == HMAC_BURST_TX && rx.rec != nullptr)
-		store_digest<dlen>(rx.rec + i * (dlen + 16), o);
+		store_digest<dlen>(rx.rec + g * (dlen + 16), o);
 	else
 		store_digest<dlen>(SIGNS ? out + (field - base) : out + i * dlen,
 		    o);

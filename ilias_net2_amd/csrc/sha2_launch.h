@@ -116,9 +116,11 @@ struct BurstArgs {
 	uint32_t cutoff, rx_start;
 	uint32_t altkey[32];	/* K' as big-endian words (the launcher turns
 				 * it into midstates; unused by the kernel) */
-	/* TX: when set, header and hash field of datagram i go to
-	 * rec + i * (hashlen + 16) -- field at +0, header at +hashlen -- and
-	 * the datagrams in base are left as they are (the host burst path) */
+	/* TX: when set, the datagrams in base are left as they are and the
+	 * lane at binned position g writes rec + g * (hashlen + 16): the hash
+	 * field (hashlen bytes, when OK), then uint32 header words as on the
+	 * wire (0 unless OK), the datagram index i and its code -- status is
+	 * then not written (the host burst path) */
 	uint8_t *rec;
 };
 hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,

@@ -1836,32 +1836,41 @@ int enqueue_burst_chunk(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 	    digest_len(hb.hash_alg) : 0;
 	WorkPool *pp = &pool;
 	s.finish = [=]() {
-		if (c_res)
+		if (c_res && !(tx && dl != 0))
 			memcpy(hb.result + lo, st_res, (size_t)n);
 		for (const std::function<void()> &c : copies)
 			c();
 		if (!tx)
 			return 0;
-		/* TX: the sealed header (and hash field) of every OK datagram
-		 * into the caller's slot (packet.n2t:384-392, :417-427) */
+		/* TX: the code of every datagram, and the sealed header (and
+		 * hash field) of every OK one into the caller's slot
+		 * (packet.n2t:384-392, :417-427) */
 		const size_t nt = std::min<size_t>(kPackThreads,
-		    std::max<size_t>(1, n >> 13));
+		    std::max<size_t>(1, n >> 12));
 		pp->run(nt, [=](size_t t) {
 			for (uint64_t j = n * t / nt; j < n * (t + 1) / nt; j++) {
+				if (dl != 0) {
+					/* record of binned position j */
+					const uint8_t *r = st_b + j * (dl + 16);
+					uint32_t w[4];
+					memcpy(w, r + dl, 16);
+					const uint64_t i = lo + w[2];
+					hb.result[i] = (uint8_t)w[3];
+					if (w[3] != NET2_PENCODE_OK)
+						continue;
+					uint8_t *dg = hb.base + hb.offsets[i];
+					memcpy(dg, w, 8);
+					memcpy(dg + 8, r, dl);
+					continue;
+				}
 				if (hb.result[lo + j] != NET2_PENCODE_OK)
 					continue;
 				uint8_t *dg = hb.base + hb.offsets[lo + j];
-				if (dl != 0) {
-					const uint8_t *r = st_b + j * (dl + 16);
-					memcpy(dg, r + dl, 8);
-					memcpy(dg + 8, r, dl);
-				} else {
-					const uint32_t sq = hb.seq_in[lo + j];
-					const uint32_t fl = hb.flags_in[lo + j];
-					for (int b = 0; b < 4; b++) {
-						dg[b] = (uint8_t)(sq >> (24 - 8 * b));
-						dg[4 + b] = (uint8_t)(fl >> (24 - 8 * b));
-					}
+				const uint32_t sq = hb.seq_in[lo + j];
+				const uint32_t fl = hb.flags_in[lo + j];
+				for (int b = 0; b < 4; b++) {
+					dg[b] = (uint8_t)(sq >> (24 - 8 * b));
+					dg[4 + b] = (uint8_t)(fl >> (24 - 8 * b));
 				}
 			}
 		});
@@ -1891,17 +1900,24 @@ int run_burst_slice(size_t didx, int ordinal, const HostBurst &hb,
 	const size_t mean = std::max<size_t>(all.start[all.nt] /
 	    std::max<uint64_t>(hi - lo, 1), 16);
 	const uint64_t per_chunk = std::max<size_t>(kChunkBytes / mean, 1);
+	/*
+	 * Chunk k is enqueued into its slot first, then chunk k - 1 (the other
+	 * slot) is waited for and its results handed over -- the TX scatter
+	 * of sealed headers runs while chunk k copies and hashes, and by the
+	 * next iteration that slot is free again.  (Draining a slot right
+	 * before reusing it put the scatter between two copies: TX 17.6 ms per
+	 * 1 M datagrams against RX's 15.2 ms.)
+	 */
 	int rc = 0, cur = 0;
 	for (uint64_t at = lo; at < hi && rc == 0;) {
 		const uint64_t end = std::min<uint64_t>(hi, at + per_chunk);
-		BurstSlot &s = b->slot[cur];
 		const double t0 = dbg_now();
-		if ((rc = s.drain()) != 0)
-			break;
+		rc = enqueue_burst_chunk(*c->pool, b->slot[cur], hb, pins, at, end);
 		const double t1 = dbg_now();
-		rc = enqueue_burst_chunk(*c->pool, s, hb, pins, at, end);
+		if (rc == 0)
+			rc = b->slot[cur ^ 1].drain();
 		if (dbg_timing())
-			fprintf(stderr, "net2 burst: drain+finish %.3f ms, enqueue "
+			fprintf(stderr, "net2 burst: enqueue %.3f ms, drain+finish "
 			    "%.3f ms (%llu datagrams)\n", t1 - t0, dbg_now() - t1,
 			    (unsigned long long)(end - at));
 		at = end;

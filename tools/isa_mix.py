@@ -50,15 +50,16 @@ KERNELS = {
     "c2": "_ZN4net23dev12fixed_kernelINS0_7Sha256TILb1ELb1ELb1ELb0EEELi0ELb1E",
     "c4": "_ZN4net23dev12fixed_kernelINS0_6Sha512ELi0ELb1E",
     "c3": "_ZN4net23dev10var_kernelINS0_7Sha256TILb1ELb1ELb1ELb0EEE",
-    "hmac": "_ZN4net23dev11hmac_kernelINS0_7Sha256TILb1ELb1ELb1ELb0EEELb1E",
-    "hmac_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha256TILb1ELb1ELb1ELb0EEELb0ELi0E",
-    "hmac512": "_ZN4net23dev11hmac_kernelINS0_8Sha512HFELb1E",
-    "hmac512_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha512HELb0ELi0E",
+    # HMAC instances: <H, PADCONST, MODE, IS384>
+    "hmac": "_ZN4net23dev11hmac_kernelINS0_7Sha256TILb1ELb1ELb1ELb0EEELb1ELi0ELb0E",
+    "hmac_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha256TILb1ELb1ELb1ELb0EEELb0ELi0ELb0E",
+    "hmac512": "_ZN4net23dev11hmac_kernelINS0_8Sha512HFELb1ELi0ELb0E",
+    "hmac512_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha512HELb0ELi0ELb0E",
     "c3_512": "_ZN4net23dev10var_kernelINS0_7Sha512VE",
-    "hmac_verify_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha256TILb1ELb1ELb0ELb0EEELb0ELi2E",
-    "hmac512_verify_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha512HELb0ELi2E",
-    "burst_rx": "_ZN4net23dev11hmac_kernelINS0_7Sha512HELb0ELi3E",
-    "burst_tx": "_ZN4net23dev11hmac_kernelINS0_7Sha512HELb0ELi4E",
+    "hmac_verify_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha256TILb1ELb1ELb0ELb0EEELb0ELi2ELb0E",
+    "hmac512_verify_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha512HELb0ELi2ELb0E",
+    "burst_rx": "_ZN4net23dev11hmac_kernelINS0_7Sha512HELb0ELi3ELb0E",
+    "burst_tx": "_ZN4net23dev11hmac_kernelINS0_7Sha512HELb0ELi4ELb0E",
 }
 
 # probe row name -> (mnemonic, operand form); form "v" = VGPR/inline-constant
