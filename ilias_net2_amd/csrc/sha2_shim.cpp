@@ -1729,6 +1729,7 @@ uint8_t *out_ptr(void *user, bool user_pinned, uint8_t *stage, bool *copy)
 /* The pinned state of each caller buffer of a host burst (looked up once). */
 struct BurstPins {
 	bool result = false, iv = false, seq = false, flags = false;
+	bool base = false;	/* the datagram buffer's start is page-locked */
 };
 
 /* What a host burst is asked to do; pointers are the caller's. */
@@ -1752,25 +1753,100 @@ struct HostBurst {
 	uint8_t *result;
 };
 
+/*
+ * The byte range [*rs, *re) (offsets from hb.base) of datagrams [lo, lo + n)
+ * when it can be DMA'd as it lies: within one page-locked allocation (both
+ * ends map to the device at the same distance) and dense -- at most a
+ * quarter more bytes than the datagrams themselves, as when the receive
+ * loop fills one pinned arena back to back.
+ */
+bool dense_pinned_range(WorkPool &pool, const HostBurst &hb, uint64_t lo,
+    uint64_t n, uint64_t *rs, uint64_t *re)
+{
+	const size_t nt = std::min<size_t>(kPackThreads,
+	    std::max<size_t>(1, n >> 14));
+	uint64_t lo_t[kPackThreads], hi_t[kPackThreads], sum_t[kPackThreads];
+	const uint64_t *off = hb.offsets + lo;
+	const uint32_t *ln = hb.lens + lo;
+	pool.run(nt, [&](size_t t) {
+		uint64_t a = UINT64_MAX, b = 0, m = 0;
+		for (uint64_t j = n * t / nt; j < n * (t + 1) / nt; j++) {
+			a = std::min<uint64_t>(a, off[j]);
+			b = std::max<uint64_t>(b, off[j] + ln[j]);
+			m += ln[j];
+		}
+		lo_t[t] = a;
+		hi_t[t] = b;
+		sum_t[t] = m;
+	});
+	uint64_t a = UINT64_MAX, b = 0, m = 0;
+	for (size_t t = 0; t < nt; t++) {
+		a = std::min(a, lo_t[t]);
+		b = std::max(b, hi_t[t]);
+		m += sum_t[t];
+	}
+	if (n == 0 || b <= a || b - a > m + m / 4)
+		return false;
+	hipPointerAttribute_t pa, pb;
+	if (hipPointerGetAttributes(&pa, hb.base + a) != hipSuccess ||
+	    hipPointerGetAttributes(&pb, hb.base + b - 1) != hipSuccess) {
+		(void)hipGetLastError();
+		return false;
+	}
+	if (pa.type != hipMemoryTypeHost || pb.type != hipMemoryTypeHost ||
+	    (const uint8_t *)pb.devicePointer - (const uint8_t *)pa.devicePointer !=
+	    (ptrdiff_t)(b - 1 - a))
+		return false;
+	*rs = a;
+	*re = b;
+	return true;
+}
+
 /* Chunk [lo, hi) of a host burst into slot s. */
 int enqueue_burst_chunk(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
     const BurstPins &pins, uint64_t lo, uint64_t hi)
 {
 	const uint64_t n = hi - lo;
-	const PackPlan plan = pack_sizes(pool, hb.lens + lo, n);
-	const size_t bytes = plan.start[plan.nt];
 	int rc;
-	if ((rc = s.reserve(bytes, n)) != 0)
-		return rc;
 	const double tp0 = dbg_now();
-	pack_fill(pool, plan, s.h_in, s.h_off, s.h_len, hb.base, hb.offsets + lo,
-	    hb.lens + lo, n);
-	if (dbg_timing())
-		fprintf(stderr, "net2 burst: pack %zu B: %.3f ms (%zu threads)\n",
-		    bytes, dbg_now() - tp0, plan.nt);
-	if (bytes != 0)
-		HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
-		    hipMemcpyHostToDevice, s.stream));
+	uint64_t rs = 0, re = 0;
+	if (pins.base && dense_pinned_range(pool, hb, lo, n, &rs, &re)) {
+		/* the chunk's datagrams lie densely in one page-locked
+		 * allocation: copied as they lie, no host pack */
+		if ((rc = s.reserve(re - rs, n)) != 0)
+			return rc;
+		const uint64_t *off = hb.offsets + lo;
+		const uint32_t *ln = hb.lens + lo;
+		uint64_t *ho = s.h_off;
+		uint32_t *hl = s.h_len;
+		const size_t nt = std::min<size_t>(kPackThreads,
+		    std::max<size_t>(1, n >> 14));
+		pool.run(nt, [=](size_t t) {
+			for (uint64_t j = n * t / nt; j < n * (t + 1) / nt; j++) {
+				ho[j] = off[j] - rs;
+				hl[j] = ln[j];
+			}
+		});
+		if (re > rs)
+			HIP_TRY(hipMemcpyAsync(s.d_in, hb.base + rs, re - rs,
+			    hipMemcpyHostToDevice, s.stream));
+		if (dbg_timing())
+			fprintf(stderr, "net2 burst: direct %llu B: %.3f ms\n",
+			    (unsigned long long)(re - rs), dbg_now() - tp0);
+	} else {
+		const PackPlan plan = pack_sizes(pool, hb.lens + lo, n);
+		const size_t bytes = plan.start[plan.nt];
+		if ((rc = s.reserve(bytes, n)) != 0)
+			return rc;
+		pack_fill(pool, plan, s.h_in, s.h_off, s.h_len, hb.base,
+		    hb.offsets + lo, hb.lens + lo, n);
+		if (dbg_timing())
+			fprintf(stderr, "net2 burst: pack %zu B: %.3f ms (%zu "
+			    "threads)\n", bytes, dbg_now() - tp0, plan.nt);
+		if (bytes != 0)
+			HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
+			    hipMemcpyHostToDevice, s.stream));
+	}
 	HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, n * 8, hipMemcpyHostToDevice,
 	    s.stream));
 	HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, n * 4, hipMemcpyHostToDevice,
@@ -1890,6 +1966,7 @@ int run_burst_slice(size_t didx, int ordinal, const HostBurst &hb,
 	std::lock_guard<std::mutex> g(b->mu);
 	HIP_TRY(hipSetDevice(ordinal));
 	BurstPins pins;
+	pins.base = is_pinned(hb.base);
 	pins.result = is_pinned(hb.result);
 	if (!hb.tx) {
 		pins.iv = hb.iv != nullptr && is_pinned(hb.iv);

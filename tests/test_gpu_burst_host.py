@@ -323,3 +323,36 @@ def test_host_burst_argument_errors(dev):
                                            None, None, None, None, 0) == 0
     assert L.net2_packet_encode_burst_host(0, None, 0, 0, None, None, None, None,
                                            None, 0, None, 0) == 0
+
+
+@pytest.mark.parametrize("gap", [0, 7, 2000])
+def test_host_burst_pinned_layouts(dev, oracle_mod, gap):
+    """Datagrams in one page-locked arena: back to back or with small gaps
+    (dense: copied to the GPU as they lie, no host pack) and with gaps as
+    large as the datagrams (sparse: packed into staging) -- the same codes,
+    sealed bytes, headers and IVs either way."""
+    from ilias_net2_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(80 + gap)
+    n, alg, ivlen = 120_000, 6, 16
+    lens = rng.choice(np.array([136, 584, 1500], dtype=np.uint32), n)
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gap)
+    total = int(offs[-1] + lens[-1])
+    buf = pinned((total,), np.uint8)
+    buf[:] = rng.integers(0, 256, total, dtype=np.uint8)
+    seq = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    flags = np.full(n, PH_SIGNED | PH_ENCRYPTED, dtype=np.uint32)
+    key = bytes(range(64))
+    o_res, o_sealed = oracle_mod.packet_encode_batch(alg, key, True, seq, flags, buf,
+                                                     offs, lens, nthreads=CPU_THREADS)
+    res = encode_host(L, alg, key, True, seq, flags, buf, offs, lens)
+    assert np.array_equal(res, o_res) and (res == OK).all()
+    assert np.array_equal(buf, o_sealed)
+    bad = np.sort(rng.choice(n, 999, replace=False))
+    buf[(offs[bad] + 70).astype(np.int64)] ^= 4      # inside the hash field
+    got = decode_host(L, rx_keys(alg, key, True), ivlen, buf, offs, lens)
+    want = oracle_mod.packet_decode_batch(alg, key, True, ivlen, buf, offs, lens,
+                                          nthreads=CPU_THREADS)
+    check_decode(got, want, ivlen)
+    assert np.array_equal(np.nonzero(got["res"])[0], bad)
