@@ -156,6 +156,29 @@ def test_no_device_fails_loudly():
     assert L.net2_sha2_ctx_update(1, ctx, buf, 64) == errno.ENODEV
     assert ctx.raw == before
     assert L.net2_sha2_ctx_final(1, buf, ctx) == errno.ENODEV
+    # host-memory packet bursts: arguments checked first, then no device
+    off = (ctypes.c_uint64 * 1)(0)
+    ln = (ctypes.c_uint32 * 1)(16)
+    key = b"k" * 64
+    keys = _lib.BurstRxKeys(6, ctypes.cast(ctypes.c_char_p(key), ctypes.c_void_p),
+                            64, 1, None, 0, 0, 0, 0)
+    assert L.net2_packet_decode_burst_host(ctypes.byref(keys), 16, buf, off, ln, 1,
+                                           buf, buf, None, None, 0) == errno.ENODEV
+    assert L.net2_packet_decode_burst_host(ctypes.byref(keys), 65, buf, off, ln, 1,
+                                           buf, buf, None, None, 0) == errno.EINVAL
+    seq = (ctypes.c_uint32 * 1)(0)
+    assert L.net2_packet_encode_burst_host(6, key, 64, 1, seq, seq, buf, off, ln, 1,
+                                           buf, 0) == errno.ENODEV
+    assert L.net2_packet_encode_burst_host(6, key, 63, 1, seq, seq, buf, off, ln, 1,
+                                           buf, 0) == errno.EINVAL
+    # the binning limits are host state; a workspace's counters need a device
+    assert L.net2_sha2_bin_limits(0, -1) == 0
+    st = _lib.BinStats()
+    assert L.net2_sha2_workspace_stats(buf, 64, ctypes.byref(st)) == errno.EINVAL
+    big = ctypes.create_string_buffer(L.net2_sha2_dev_var_workspace(0) + 8)
+    aligned = (ctypes.addressof(big) + 7) & ~7
+    assert L.net2_sha2_workspace_stats(aligned, L.net2_sha2_dev_var_workspace(0),
+                                       ctypes.byref(st)) == errno.ENODEV
 
 
 @pytest.mark.skipif(_lib.device_count() > 0, reason="a GPU is present")
