@@ -804,6 +804,10 @@ def extra_configs(args, dev, probe, ws=1, rank=0, label=None):
     if ws > 1:
         out["e2e"] = e2e_rate(steps=10, warmup=3, ws=ws, dev=dev,
                               dist_backend=args.dist_backend, label=label)
+        # the per-datagram path from host memory on every GPU at once
+        out["burst_rx_e2e"] = burst_e2e_rate("rx", steps=6, warmup=2, ws=ws, dev=dev,
+                                             dist_backend=args.dist_backend,
+                                             label=label)
         return out
     for name in ("c3", "c4"):
         r = time_device_config(name, dev, args.steps, min(args.warmup, 10),
@@ -929,7 +933,8 @@ def _e2e_timed(steps, warmup, n, length, ws, dev, dist_backend, numa,
             "host_buffers_numa_local": numa}
 
 
-def burst_e2e_rate(kind, steps=8, warmup=2, n=1 << 20, memory="pinned"):
+def burst_e2e_rate(kind, steps=8, warmup=2, n=1 << 20, memory="pinned", ws=1,
+                   dev=None, dist_backend="nccl", label="1 GPU"):
     """The burst configs end to end from host memory (VERDICT round 4 item
     1): 1 M wire datagrams of {136, 584, 1500} B (8-byte header, 64-byte
     HMAC-SHA512 field, payload; every one PH_SIGNED|PH_ENCRYPTED) in host
@@ -937,7 +942,8 @@ def burst_e2e_rate(kind, steps=8, warmup=2, n=1 << 20, memory="pinned"):
     IVs back to host memory) or net2_packet_encode_burst_host (TX: header
     and HMAC field sealed into the caller's buffer) on this process's GPU
     (max_devices 1).  The datagrams are sealed once, untimed, before the RX
-    steps."""
+    steps.  At N>1 every rank does the same on its own GPU at once (timed
+    between barriers, max over ranks; value = all ranks' datagrams)."""
     import numpy as np
     import torch
     from ilias_net2_amd import _lib
@@ -981,22 +987,33 @@ def burst_e2e_rate(kind, steps=8, warmup=2, n=1 << 20, memory="pinned"):
     step = rx if kind == "rx" else tx
     for _ in range(warmup):
         step()
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
+    if ws > 1:
+        dist.barrier()
     ms = (time.perf_counter() - t0) * 1e3 / steps
+    if ws > 1:
+        t = torch.tensor([ms], dtype=torch.float64,
+                         device=dev if dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t[0])
     assert int((res != 0).sum()) == 0, f"burst {kind}: datagrams not OK"
     out_bytes = n * (1 + 16 + 8) if kind == "rx" else n * (1 + 8 + 64)
     r = {"metric": ("datagrams decoded/s" if kind == "rx" else "datagrams encoded/s") +
                    f", 1M x {{136,584,1500}} B wire datagrams from {memory} host memory, "
                    "end to end (pack, H2D, HMAC-SHA512" +
                    (" verify + 16-B IVs" if kind == "rx" else " seal") +
-                   ", results to host memory), 1 GPU",
-         "value": round(n / (ms / 1e3), 1), "unit": "datagrams/s", "steps": steps,
+                   f", results to host memory), {label}",
+         "value": round(n * ws / (ms / 1e3), 1), "unit": "datagrams/s", "steps": steps,
+         "n_gpus": ws,
          "ms_per_step": round(ms, 3),
          "workload": f"net2_packet_{'decode' if kind == 'rx' else 'encode'}_burst_host, "
                      f"{memory} datagram buffer and result arrays, max_devices 1",
-         "h2d_GBps": round(total / (ms / 1e3) / 1e9, 2),
+         "h2d_GBps" if ws == 1 else "h2d_GBps_per_gpu": round(total / (ms / 1e3) / 1e9, 2),
          "host_bytes_per_step": {"datagrams_in": total, "results_out": out_bytes}}
     del data, res, iv, oseq, ofl
     return r
