@@ -101,6 +101,12 @@ def main():
                           f"event_ms={kms if kms is None else round(kms, 4)}",
                           flush=True)
         os.environ.pop(a.knob, None)
+        from ilias_net2_amd import _lib
+        torch.cuda.synchronize(dev)
+        for k, w in enumerate(wss):     # did every binning launch bin?
+            if w is not None:
+                print(f"{name} workspace {k}: "
+                      f"{_lib.workspace_stats(w.data_ptr(), w.numel() * 4)}", flush=True)
         del inp, outs, wss
         torch.cuda.empty_cache()
 
