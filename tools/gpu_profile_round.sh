@@ -15,4 +15,13 @@ for c in $PC; do
   cp profiles/pmc_$c.json gpurun_out/pmc_$c.json
   cp profiles/$ROUND/kernel_stats_$c.csv gpurun_out/profiles_$ROUND/ 2>/dev/null
 done
+# the raw per-dispatch CSVs are folded now: drop them (after every config is
+# summarised -- pmc_hmac_* also matches pmc_hmac_mtu_*), so what comes back
+# stays under gpurun's 64 MiB
+for c in $PC; do
+  for pass in SQ_INSTS_VALU SQ_ACTIVE_INST_VALU FETCH_SIZE WRITE_SIZE SQ_INSTS_SALU; do
+    rm -rf gpurun_out/pmc_${c}_$pass
+  done
+  rm -f gpurun_out/prof_$c/run_kernel_trace.csv
+done
 exit 0

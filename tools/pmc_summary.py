@@ -39,8 +39,9 @@ KERNEL = {"c2": "fixed_kernel<net2::dev::Sha256", "c4": "fixed_kernel<net2::dev:
 # the timed kernel's HMAC mode (the template's last argument), where the
 # config also runs another mode once, untimed: the signing pass before a
 # verify config, the encode before burst RX
-MODE = {"hmac_verify_mtu": ", 2>", "hmac512_verify_mtu": ", 2>", "burst_rx": ", 3>",
-        "burst_tx": ", 4>"}
+# (hmac_kernel<H, PADCONST, MODE, IS384>: these configs run IS384 = false)
+MODE = {"hmac_verify_mtu": ", 2, false>", "hmac512_verify_mtu": ", 2, false>",
+        "burst_rx": ", 3, false>", "burst_tx": ", 4, false>"}
 
 
 def matches(name, cfg):
