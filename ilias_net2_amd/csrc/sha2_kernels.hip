@@ -1212,9 +1212,12 @@ __device__ __forceinline__ void hmac_item(uint64_t g,
 		return;
 	uint32_t o[16];
 	H::out_words(st, o, is384);
-	/* SIGN / VERIFY: the hash field, found again from the descriptor (one
-	 * L2-hot load) rather than held in two VGPRs across the hash: the
-	 * datagram's start, past the header in the burst modes */
+	/* SIGN / VERIFY: the hash field, found again from the descriptor
+	 * rather than held in two VGPRs across the hash: the datagram's start,
+	 * past the header in the burst modes.  Its line has mostly left L2 by
+	 * now (burst RX reads ~115 B more per datagram than round 4,
+	 * profiles/pmc_burst_rx.json): HBM bytes, no time on this VALU-bound
+	 * kernel */
 	const uint8_t *field = MODE == HMAC_DIGESTS ? nullptr :
 	    base + offsets[i] + (MODE == HMAC_BURST_RX || MODE == HMAC_BURST_TX ?
 	    8 : 0);
