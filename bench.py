@@ -70,6 +70,10 @@ CONFIGS = {
                      workload="1M x {136,584,1500} B wire datagrams, net2_packet_decode_burst: header, HMAC-SHA512 verify, 16-B IVs (8f row 3', RX)"),
     "burst_tx": dict(alg=6, kind="burst_tx", n=1 << 20, length=None, ivlen=16,
                      workload="1M x {136,584,1500} B wire datagrams, net2_packet_encode_burst: header + HMAC-SHA512 field (8f row 3', TX)"),
+    # the same burst under HMAC-SHA256 (a connection that negotiated it; the
+    # SHA-256 kernels' RX mode, not a BASELINE config)
+    "burst_rx256": dict(alg=4, kind="burst_rx", n=1 << 20, length=None, ivlen=16,
+                        workload="1M x {136,584,1500} B wire datagrams, net2_packet_decode_burst: header, HMAC-SHA256 verify, 16-B IVs (8f row 3', RX)"),
     "ph_iv": dict(alg=1, kind="ph_iv", n=1 << 20, length=16,
                   workload="1M packet headers -> 16-byte IVs, net2_ph_to_iv_dev (8f row 3)"),
 }
@@ -371,12 +375,15 @@ def load_isa_mix(config_name):
     return mix["configs"].get(config_name)
 
 
-def device_step(name, inp, out, ws_buf, stream, unbinned=False):
+def device_step(name, inp, out, ws_buf, stream, unbinned=False, kind=None):
     """One step of a device-resident config: one pass of the hot path over
     the whole batch (one launch, plus the binning launches of the variable
-    layout)."""
+    layout).  kind overrides the config's (the untimed encode of an RX
+    burst, under the config's own algorithm)."""
     from ilias_net2_amd import batch, _lib
-    cfg = CONFIGS[name]
+    cfg = dict(CONFIGS[name])
+    if kind is not None:
+        cfg["kind"] = kind
     L = _lib.lib()
     n, alg = inp["n"], cfg["alg"]
     kbuf = HMAC_KEY[:DLEN[alg]] if alg >= 4 else b""
@@ -441,7 +448,7 @@ def time_device_config(name, dev, steps, warmup, prewarm_ms, ws=1, rank=0,
                              dtype=torch.uint8, device=dev)
     if cfg["kind"] == "burst_rx":
         # encode once (untimed), so every datagram verifies and gets its IV
-        device_step("burst_tx", inp, out, ws_buf, stream)()
+        device_step(name, inp, out, ws_buf, stream, kind="burst_tx")()
         torch.cuda.synchronize(dev)
         assert int((out != 0).sum()) == 0, "burst encode failed"
     if cfg["kind"] == "dgram_verify":

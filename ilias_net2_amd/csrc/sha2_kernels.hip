@@ -89,8 +89,8 @@ struct Sha256T {
  * Every SHA-256 kernel takes the asm rounds, the two-block loop and the
  * pair loop (fixed kernel: 92 VGPRs; variable-length kernel: 96, C3 +0.7 %
  * with the pair loop, profiles/round1/var_pair_ab.txt; C3 452 against
- * 463 us with the asm rounds, profiles/round2/var_asm_ab.txt).  The RX
- * verify kernel drops the pair loop (NoPair below).
+ * 463 us with the asm rounds, profiles/round2/var_asm_ab.txt); the HMAC
+ * kernels in every mode (launch_hmac_var_mode).
  */
 typedef Sha256T<true, true, true> Sha256;	/* fixed, variable, HMAC */
 typedef Sha256 Sha256V;
@@ -2032,6 +2032,10 @@ __global__ __launch_bounds__(256) void bin_onepass_kernel(
 		 * histogram is known to add up to n */
 		constexpr int PER = NET2_SHA2_NBINS / 256;
 		const int lane = (int)__lane_id(), wave = (int)(threadIdx.x / 64);
+		/* (The histogram read with coalesced 8-byte loads staged through
+		 * LDS, one request per line per workgroup instead of eight:
+		 * 0.4 us slower to the bases -- the read is one round trip, not
+		 * contention; profiles/round5/bin_probe_coalesced_read.txt.) */
 		uint32_t v[PER], sum = 0;
 		uint64_t sum64 = 0;
 #pragma unroll
@@ -2455,13 +2459,11 @@ hipError_t net2_launch_var(int alg, const uint8_t *base,
 		    lens, ws, launch, n, out, dlen, is384);
 	return hipGetLastError();
 }
-/* H without the pair loop: the VERIFY kernel measured 1.5 % faster without
- * it (110 -> fewer VGPRs), the digest kernels 0.5-2 % faster with it
- * (profiles/round1/hmac_pair_ab.txt). */
-template <class H> struct NoPair { typedef H type; };
-template <bool A, bool U, bool P> struct NoPair<Sha256T<A, U, P> > {
-	typedef Sha256T<A, U, false> type;
-};
+/* Every mode takes H's pair loop.  (Until round 5 the SHA-256 VERIFY and
+ * BURST_RX kernels dropped it: 1.5 % faster in round 1, when the key pass
+ * held their VGPRs at 110.  With the midstates from the host they measured
+ * +4.3 to +5.3 % (verify) and +2.9 to +3.3 % (burst RX) with it,
+ * profiles/round5/ab_pairall_box*.txt.) */
 
 template <class H, bool IS384>
 static void launch_hmac_var_mode(int mode, unsigned grid, hipStream_t s,
@@ -2473,11 +2475,11 @@ static void launch_hmac_var_mode(int mode, unsigned grid, hipStream_t s,
 		hmac_kernel<H, false, HMAC_SIGN, IS384><<<grid, 256, 0, s>>>(base,
 		    offsets, lens, ws, launch, 0, 0, n, out, hm, pad, rx);
 	else if (mode == HMAC_VERIFY)
-		hmac_kernel<typename NoPair<H>::type, false, HMAC_VERIFY, IS384>
+		hmac_kernel<H, false, HMAC_VERIFY, IS384>
 		    <<<grid, 256, 0, s>>>(base, offsets, lens, ws, launch, 0, 0, n,
 		    out, hm, pad, rx);
 	else if (mode == HMAC_BURST_RX)
-		hmac_kernel<typename NoPair<H>::type, false, HMAC_BURST_RX, IS384>
+		hmac_kernel<H, false, HMAC_BURST_RX, IS384>
 		    <<<grid, 256, 0, s>>>(base, offsets, lens, ws, launch, 0, 0, n,
 		    out, hm, pad, rx);
 	else if (mode == HMAC_BURST_TX)

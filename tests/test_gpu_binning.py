@@ -341,7 +341,13 @@ def test_overwritten_workspace_is_detected(dev, oracle_mod):
     assert st["prepared"] and st["unprepared"] == 1 and st["binned"] == 3, st
     assert (np.diff(_blocks(lens, 1)[_order(ws, L, n)]) <= 0).all()
     # 2. barrier words that decide GO at the first arrival: whatever the
-    # workgroups then read, the digests stay right
+    # workgroups then read, the digests stay right.  (The early decision also
+    # bumps the epoch early: a workgroup that starts only after it reads the
+    # next parity, joins that parity's barrier alone and waits out the
+    # timeout -- an ABORT, counted, its counts a mismatch of the launch after.
+    # Rare -- tools/forge_probe.py: none in 40 forged launches -- and only
+    # with forged words: an honest barrier decides after every workgroup has
+    # read the epoch.)
     for _ in range(3):
         base = ctl0 + (epoch() & 1) * 1024
         ws[base + 512] = min(G, 16) - 1     # top counter: one arrival short
@@ -349,7 +355,18 @@ def test_overwritten_workspace_is_detected(dev, oracle_mod):
         run()
         run()
     st = _stats(L, ws)
-    assert st["aborts"] == 0, st
+    assert st["aborts"] <= 3, st
+    # 3. the caller stops overwriting: every launch bins again, no fallback
+    for _ in range(3):
+        run()
+    after = _stats(L, ws)
+    run()
+    run()
+    final = _stats(L, ws)
+    assert final["binned"] == after["binned"] + 2, (after, final)
+    assert (final["aborts"], final["mismatches"]) == (after["aborts"],
+                                                    after["mismatches"]), final
+    assert (np.diff(_blocks(lens, 1)[_order(ws, L, n)]) <= 0).all()
 
 
 def test_burst_workspace_reused_across_sizes(dev, oracle_mod):
