@@ -171,11 +171,10 @@ struct Slot {
 	hipEvent_t done = nullptr;
 	bool busy = false;
 	uint8_t *h_in = nullptr, *h_dig = nullptr;
+	/* a chunk's offsets (8 n bytes) then lengths (4 n): one copy */
 	uint64_t *h_off = nullptr;
-	uint32_t *h_len = nullptr;
 	uint8_t *d_in = nullptr, *d_dig = nullptr;
 	uint64_t *d_off = nullptr;
-	uint32_t *d_len = nullptr;
 	uint32_t *d_ws = nullptr;
 	size_t cap_in = 0, cap_n = 0;
 	/* digests of the chunk in flight go back to the caller here */
@@ -187,18 +186,15 @@ struct Slot {
 		if (h_in) (void)hipHostFree(h_in);
 		if (h_dig) (void)hipHostFree(h_dig);
 		if (h_off) (void)hipHostFree(h_off);
-		if (h_len) (void)hipHostFree(h_len);
 		if (d_in) (void)hipFree(d_in);
 		if (d_dig) (void)hipFree(d_dig);
 		if (d_off) (void)hipFree(d_off);
-		if (d_len) (void)hipFree(d_len);
 		if (d_ws) (void)hipFree(d_ws);
 		h_in = h_dig = nullptr;
 		h_off = nullptr;
-		h_len = nullptr;
 		d_in = d_dig = nullptr;
 		d_off = nullptr;
-		d_len = d_ws = nullptr;
+		d_ws = nullptr;
 		cap_in = cap_n = 0;
 	}
 
@@ -229,14 +225,11 @@ struct Slot {
 			    hipHostMallocDefault));
 		HIP_TRY(hipHostMalloc((void **)&h_dig, n * 64,
 		    hipHostMallocDefault));
-		HIP_TRY(hipHostMalloc((void **)&h_off, n * 8,
-		    hipHostMallocDefault));
-		HIP_TRY(hipHostMalloc((void **)&h_len, n * 4,
+		HIP_TRY(hipHostMalloc((void **)&h_off, n * 12,
 		    hipHostMallocDefault));
 		HIP_TRY(hipMalloc((void **)&d_in, in));
 		HIP_TRY(hipMalloc((void **)&d_dig, n * 64));
-		HIP_TRY(hipMalloc((void **)&d_off, n * 8));
-		HIP_TRY(hipMalloc((void **)&d_len, n * 4));
+		HIP_TRY(hipMalloc((void **)&d_off, n * 12));
 		HIP_TRY(hipMalloc((void **)&d_ws,
 		    (NET2_BIN_WS_WORDS + n) * sizeof(uint32_t)));
 		/* prepared once, so the first variable-layout chunk bins too */
@@ -701,20 +694,19 @@ int enqueue_chunk(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
 		    kout, s.stream));
 	} else {
 		const double tg0 = dbg_now();
-		pack_fill(pool, plan, s.h_in, s.h_off, s.h_len, base, offsets + lo,
-		    lens + lo, n);
+		pack_fill(pool, plan, s.h_in, s.h_off, (uint32_t *)(s.h_off + n),
+		    base, offsets + lo, lens + lo, n);
 		if (dbg_timing())
 			fprintf(stderr, "net2: pack %zu B, %llu packets: %.3f ms\n",
 			    bytes, (unsigned long long)n, dbg_now() - tg0);
 		if (bytes != 0)
 			HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
 			    hipMemcpyHostToDevice, s.stream));
-		HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, n * 8,
+		HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, n * 12,
 		    hipMemcpyHostToDevice, s.stream));
-		HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, n * 4,
-		    hipMemcpyHostToDevice, s.stream));
-		HIP_TRY(net2_launch_var(alg, s.d_in, s.d_off, s.d_len, n,
-		    kout, n >= 4096 ? s.d_ws : nullptr, s.stream));
+		HIP_TRY(net2_launch_var(alg, s.d_in, s.d_off,
+		    (const uint32_t *)(s.d_off + n), n, kout,
+		    n >= 4096 ? s.d_ws : nullptr, s.stream));
 	}
 	if (!direct)
 		HIP_TRY(hipMemcpyAsync(host_dig, s.d_dig, (size_t)n * dl,
@@ -1594,12 +1586,23 @@ struct BurstSlot {
 	hipEvent_t done = nullptr;
 	bool busy = false;
 	uint8_t *h_in = nullptr, *h_out = nullptr;
-	uint64_t *h_off = nullptr;
-	uint32_t *h_len = nullptr, *h_hdr = nullptr;
-	uint8_t *d_in = nullptr, *d_ws = nullptr;
-	uint64_t *d_off = nullptr;
-	uint32_t *d_len = nullptr, *d_hdr = nullptr;
+	/* a chunk's per-datagram metadata, one block so it is one copy:
+	 * offsets (8 n), lengths (4 n), TX headers (8 n) -- see Meta */
+	uint8_t *h_meta = nullptr;
+	uint8_t *d_in = nullptr, *d_ws = nullptr, *d_meta = nullptr;
 	size_t cap_in = 0, cap_n = 0;
+
+	/* The metadata arrays of an n-datagram chunk inside a meta block. */
+	struct Meta {
+		uint64_t *off;
+		uint32_t *len, *hdr;
+		Meta(uint8_t *m, size_t n) : off((uint64_t *)m),
+		    len((uint32_t *)(m + 8 * n)), hdr((uint32_t *)(m + 12 * n)) {}
+	};
+	static size_t meta_bytes(size_t n, bool tx)
+	{
+		return n * (tx ? 20 : 12);
+	}
 	/* run once the chunk's kernels are done: results to the caller */
 	std::function<int()> finish;
 
@@ -1614,20 +1617,12 @@ struct BurstSlot {
 	{
 		if (h_in) (void)hipHostFree(h_in);
 		if (h_out) (void)hipHostFree(h_out);
-		if (h_off) (void)hipHostFree(h_off);
-		if (h_len) (void)hipHostFree(h_len);
-		if (h_hdr) (void)hipHostFree(h_hdr);
+		if (h_meta) (void)hipHostFree(h_meta);
 		if (d_in) (void)hipFree(d_in);
 		if (d_ws) (void)hipFree(d_ws);
-		if (d_off) (void)hipFree(d_off);
-		if (d_len) (void)hipFree(d_len);
-		if (d_hdr) (void)hipFree(d_hdr);
-		h_in = h_out = nullptr;
-		h_off = nullptr;
-		h_len = h_hdr = nullptr;
-		d_in = d_ws = nullptr;
-		d_off = nullptr;
-		d_len = d_hdr = nullptr;
+		if (d_meta) (void)hipFree(d_meta);
+		h_in = h_out = h_meta = nullptr;
+		d_in = d_ws = d_meta = nullptr;
 		cap_in = cap_n = 0;
 	}
 
@@ -1647,16 +1642,10 @@ struct BurstSlot {
 		HIP_TRY(hipHostMalloc((void **)&h_in, in, hipHostMallocDefault));
 		HIP_TRY(hipHostMalloc((void **)&h_out, out_bytes(n),
 		    hipHostMallocDefault));
-		HIP_TRY(hipHostMalloc((void **)&h_off, n * 8,
-		    hipHostMallocDefault));
-		HIP_TRY(hipHostMalloc((void **)&h_len, n * 4,
-		    hipHostMallocDefault));
-		HIP_TRY(hipHostMalloc((void **)&h_hdr, n * 8,
+		HIP_TRY(hipHostMalloc((void **)&h_meta, meta_bytes(n, true),
 		    hipHostMallocDefault));
 		HIP_TRY(hipMalloc((void **)&d_in, in));
-		HIP_TRY(hipMalloc((void **)&d_off, n * 8));
-		HIP_TRY(hipMalloc((void **)&d_len, n * 4));
-		HIP_TRY(hipMalloc((void **)&d_hdr, n * 8));
+		HIP_TRY(hipMalloc((void **)&d_meta, meta_bytes(n, true)));
 		HIP_TRY(hipMalloc((void **)&d_ws, burst_layout(n, nullptr,
 		    nullptr)));
 		/* its binning area prepared once, so the first chunk bins */
@@ -1810,15 +1799,22 @@ int enqueue_burst_chunk(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 	int rc;
 	const double tp0 = dbg_now();
 	uint64_t rs = 0, re = 0;
-	if (pins.base && dense_pinned_range(pool, hb, lo, n, &rs, &re)) {
+	const bool direct = pins.base && dense_pinned_range(pool, hb, lo, n, &rs,
+	    &re);
+	PackPlan plan;
+	if (!direct)
+		plan = pack_sizes(pool, hb.lens + lo, n);
+	const size_t bytes = direct ? re - rs : plan.start[plan.nt];
+	if ((rc = s.reserve(bytes, n)) != 0)
+		return rc;
+	const BurstSlot::Meta hm(s.h_meta, n), dm(s.d_meta, n);
+	if (direct) {
 		/* the chunk's datagrams lie densely in one page-locked
 		 * allocation: copied as they lie, no host pack */
-		if ((rc = s.reserve(re - rs, n)) != 0)
-			return rc;
 		const uint64_t *off = hb.offsets + lo;
 		const uint32_t *ln = hb.lens + lo;
-		uint64_t *ho = s.h_off;
-		uint32_t *hl = s.h_len;
+		uint64_t *ho = hm.off;
+		uint32_t *hl = hm.len;
 		const size_t nt = std::min<size_t>(kPackThreads,
 		    std::max<size_t>(1, n >> 14));
 		pool.run(nt, [=](size_t t) {
@@ -1827,18 +1823,14 @@ int enqueue_burst_chunk(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 				hl[j] = ln[j];
 			}
 		});
-		if (re > rs)
-			HIP_TRY(hipMemcpyAsync(s.d_in, hb.base + rs, re - rs,
+		if (bytes != 0)
+			HIP_TRY(hipMemcpyAsync(s.d_in, hb.base + rs, bytes,
 			    hipMemcpyHostToDevice, s.stream));
 		if (dbg_timing())
-			fprintf(stderr, "net2 burst: direct %llu B: %.3f ms\n",
-			    (unsigned long long)(re - rs), dbg_now() - tp0);
+			fprintf(stderr, "net2 burst: direct %zu B: %.3f ms\n", bytes,
+			    dbg_now() - tp0);
 	} else {
-		const PackPlan plan = pack_sizes(pool, hb.lens + lo, n);
-		const size_t bytes = plan.start[plan.nt];
-		if ((rc = s.reserve(bytes, n)) != 0)
-			return rc;
-		pack_fill(pool, plan, s.h_in, s.h_off, s.h_len, hb.base,
+		pack_fill(pool, plan, s.h_in, hm.off, hm.len, hb.base,
 		    hb.offsets + lo, hb.lens + lo, n);
 		if (dbg_timing())
 			fprintf(stderr, "net2 burst: pack %zu B: %.3f ms (%zu "
@@ -1847,10 +1839,13 @@ int enqueue_burst_chunk(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 			HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
 			    hipMemcpyHostToDevice, s.stream));
 	}
-	HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, n * 8, hipMemcpyHostToDevice,
-	    s.stream));
-	HIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, n * 4, hipMemcpyHostToDevice,
-	    s.stream));
+	if (hb.tx) {
+		memcpy(hm.hdr, hb.seq_in + lo, (size_t)n * 4);
+		memcpy(hm.hdr + n, hb.flags_in + lo, (size_t)n * 4);
+	}
+	/* offsets, lengths (and TX headers): one copy */
+	HIP_TRY(hipMemcpyAsync(s.d_meta, s.h_meta,
+	    BurstSlot::meta_bytes(n, hb.tx), hipMemcpyHostToDevice, s.stream));
 
 	/* staged results: [code n][IV n x ivlen | records][seq n][flags n] */
 	uint8_t *st_res = s.h_out;
@@ -1875,7 +1870,7 @@ int enqueue_burst_chunk(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 		    nullptr || (k_fl = out_ptr(hb.flags_out + lo, pins.flags,
 		    st_fl, &c_fl)) == nullptr))
 			return EIO;
-		if ((rc = decode_burst(hb.keys, hb.ivlen, s.d_in, s.d_off, s.d_len,
+		if ((rc = decode_burst(hb.keys, hb.ivlen, s.d_in, dm.off, dm.len,
 		    n, k_res, k_iv, (uint32_t *)k_sq, (uint32_t *)k_fl, s.d_ws,
 		    s.stream, true)) != 0)
 			return rc;
@@ -1889,10 +1884,6 @@ int enqueue_burst_chunk(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 			copies.push_back([=]() { memcpy(hb.flags_out + lo, st_fl,
 			    (size_t)n * 4); });
 	} else {
-		memcpy(s.h_hdr, hb.seq_in + lo, (size_t)n * 4);
-		memcpy(s.h_hdr + n, hb.flags_in + lo, (size_t)n * 4);
-		HIP_TRY(hipMemcpyAsync(s.d_hdr, s.h_hdr, n * 8,
-		    hipMemcpyHostToDevice, s.stream));
 		const bool keyed = hb.hash_alg != NET2_HASH_NIL;
 		void *recd = nullptr;
 		if (keyed && (hipHostGetDevicePointer(&recd, st_b, 0) != hipSuccess ||
@@ -1901,7 +1892,7 @@ int enqueue_burst_chunk(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 			return EIO;
 		}
 		if ((rc = encode_burst(hb.hash_alg, hb.hash_key, hb.hash_keylen,
-		    hb.enc_alg, s.d_hdr, s.d_hdr + n, s.d_in, s.d_off, s.d_len, n,
+		    hb.enc_alg, dm.hdr, dm.hdr + n, s.d_in, dm.off, dm.len, n,
 		    k_res, s.d_ws, s.stream, (uint8_t *)recd)) != 0)
 			return rc;
 	}

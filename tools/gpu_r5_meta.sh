@@ -1,0 +1,10 @@
+set -u
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_burst_host.py tests/test_gpu_multidev.py tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_gpu_binning.py > gpurun_out/t_meta.log 2>&1; rc=$?; tail -3 gpurun_out/t_meta.log; [ $rc -ne 0 ] && exit $rc
+: > gpurun_out/meta_ab.txt
+for r in 1 2; do for l in pairall default; do
+  if [ $l = default ]; then unset NET2_SHA2_LIB; else export NET2_SHA2_LIB=$PWD/tools/ab/$l.so; fi
+  for k in tx rx; do for m in pinned pageable; do timeout -k 10 120 python tools/burst_e2e.py $k $m > gpurun_out/be2e.json 2>/dev/null || exit 1; python3 -c "import json; d=json.loads(open('gpurun_out/be2e.json').read().strip().splitlines()[-1]); print('$r $l $k $m', round(d['value']/1e6,2), d['ms_per_step'])" >> gpurun_out/meta_ab.txt; done; done
+  timeout -k 10 300 python tools/e2e_var.py > gpurun_out/e2e_var.txt 2>&1 || exit 1; echo "$r $l $(tail -1 gpurun_out/e2e_var.txt)" >> gpurun_out/meta_ab.txt
+done; done
+cat gpurun_out/meta_ab.txt
