@@ -6,7 +6,7 @@ set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 ROUND=${ROUND:-round3}
-PC="${PCFGS:-c2 c4 c3 c3_512 hmac hmac_mtu hmac512 hmac512_mtu hmac_verify_mtu hmac512_verify_mtu burst_rx burst_tx ph_iv}"
+PC="${PCFGS:-c2 c4 c3 c3_512 hmac hmac_mtu hmac512 hmac512_mtu hmac_verify_mtu hmac512_verify_mtu burst_rx burst_tx burst_rx256 ph_iv}"
 CFGS="$PC" bash tools/gpu_profile.sh
 rc=$?; echo "profile rc=$rc"; [ $rc -ne 0 ] && exit $rc
 mkdir -p gpurun_out/profiles_$ROUND

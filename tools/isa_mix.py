@@ -56,10 +56,11 @@ KERNELS = {
     "hmac512": "_ZN4net23dev11hmac_kernelINS0_8Sha512HFELb1ELi0ELb0E",
     "hmac512_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha512HELb0ELi0ELb0E",
     "c3_512": "_ZN4net23dev10var_kernelINS0_7Sha512VE",
-    "hmac_verify_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha256TILb1ELb1ELb0ELb0EEELb0ELi2ELb0E",
+    "hmac_verify_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha256TILb1ELb1ELb1ELb0EEELb0ELi2ELb0E",
     "hmac512_verify_mtu": "_ZN4net23dev11hmac_kernelINS0_7Sha512HELb0ELi2ELb0E",
     "burst_rx": "_ZN4net23dev11hmac_kernelINS0_7Sha512HELb0ELi3ELb0E",
     "burst_tx": "_ZN4net23dev11hmac_kernelINS0_7Sha512HELb0ELi4ELb0E",
+    "burst_rx256": "_ZN4net23dev11hmac_kernelINS0_7Sha256TILb1ELb1ELb1ELb0EEELb0ELi3ELb0E",
 }
 
 # probe row name -> (mnemonic, operand form); form "v" = VGPR/inline-constant

@@ -35,13 +35,14 @@ KERNEL = {"c2": "fixed_kernel<net2::dev::Sha256", "c4": "fixed_kernel<net2::dev:
           "hmac512": "hmac_kernel<net2::dev::Sha512", "hmac512_mtu": "hmac_kernel<net2::dev::Sha512",
           "hmac_verify_mtu": "hmac_kernel<net2::dev::Sha256",
           "hmac512_verify_mtu": "hmac_kernel<net2::dev::Sha512",
-          "burst_rx": "hmac_kernel<net2::dev::Sha512", "burst_tx": "hmac_kernel<net2::dev::Sha512"}
+          "burst_rx": "hmac_kernel<net2::dev::Sha512", "burst_tx": "hmac_kernel<net2::dev::Sha512",
+          "burst_rx256": "hmac_kernel<net2::dev::Sha256"}
 # the timed kernel's HMAC mode (the template's last argument), where the
 # config also runs another mode once, untimed: the signing pass before a
 # verify config, the encode before burst RX
 # (hmac_kernel<H, PADCONST, MODE, IS384>: these configs run IS384 = false)
 MODE = {"hmac_verify_mtu": ", 2, false>", "hmac512_verify_mtu": ", 2, false>",
-        "burst_rx": ", 3, false>", "burst_tx": ", 4, false>"}
+        "burst_rx": ", 3, false>", "burst_tx": ", 4, false>", "burst_rx256": ", 3, false>"}
 
 
 def matches(name, cfg):
