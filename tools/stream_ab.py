@@ -61,8 +61,9 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--alternations", type=int, default=3)
-    ap.add_argument("--knob", default="NET2_FIXED_OCC",
-                    help="environment variable the library reads per launch")
+    ap.add_argument("--knob", default="NET2_KNOB",
+                    help="environment variable an A/B build reads per launch "
+                    "(the shipped library reads none; used with --values)")
     ap.add_argument("--values", default="",
                     help="comma list of values of --knob to A/B")
     a = ap.parse_args()
