@@ -611,6 +611,17 @@ def rooflines(name, launch_ms, per_launch, sclk_mhz=None):
                     "frac_at_timed_sclk": round(floor_ms * 2400.0 / sclk_mhz / launch_ms, 4),
                     "timed_sclk_mhz": sclk_mhz} if sclk_mhz else {}),
                 "source": "profiles/isa_mix.json (mixed-stream model) x profiles/round1/valu_bank_seq_probe.json (cost)"}
+            step = pmc.get("step_valu_wave_instr")
+            if step and step > instr and sclk_mhz:
+                # the same floor over the VALU work of every launch of the
+                # step (binning, the burst final kernel's IV derivation),
+                # priced at the same cost: what the step could take
+                sfl = step / 1024 * m / (sclk_mhz * 1e6) * 1e3
+                valu["issue_floor"]["step"] = {
+                    "instr_per_step": step,
+                    "kernels": sorted(pmc.get("step_kernels_valu", {})),
+                    "floor_ms_at_timed_sclk": round(sfl, 4),
+                    "frac_at_timed_sclk": round(sfl / launch_ms, 4)}
     return roof, valu
 
 

@@ -66,6 +66,34 @@ def per_dispatch(path, cfg):
     return out, list(durs.values())
 
 
+def step_kernels(path, cfg, counter="SQ_INSTS_VALU"):
+    """The library's kernels that run once per step beside the dominant one
+    (binning, the burst final kernel): {short name: (dispatches, median
+    counter per dispatch)}, kernels dispatched about as often as the
+    dominant one only (not the untimed set-up launches)."""
+    vals, names = {}, {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            nm = r["Kernel_Name"]
+            if "net2::dev::" not in nm or r["Counter_Name"] != counter:
+                continue
+            d = r["Dispatch_Id"]
+            vals[(nm, d)] = vals.get((nm, d), 0.0) + float(r["Counter_Value"])
+    for (nm, d), v in vals.items():
+        names.setdefault(nm, []).append(v)
+    dom = [v for nm, v in names.items() if matches(nm, cfg)]
+    if not dom:
+        return {}
+    ndom = len(dom[0])
+    out = {}
+    for nm, v in names.items():
+        if len(v) >= 0.9 * ndom:
+            short = nm.split("(")[0].replace("void ", "").replace("net2::dev::", "")
+            out[short] = {"dispatches": len(v), "median_per_dispatch": statistics.median(v),
+                          "dominant": matches(nm, cfg)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cfg", required=True, choices=sorted(KERNEL))
@@ -125,6 +153,13 @@ def main():
         res["correction"] = "FETCH_SIZE*1024*2 (gfx950 16B/lane half-count) + WRITE_SIZE*1024"
     if "SQ_INSTS_VALU" in med:
         res["valu_wave_instr_per_launch"] = med["SQ_INSTS_VALU"]
+        path = os.path.join(args.src, f"pmc_{args.cfg}_SQ_INSTS_VALU", "run_counter_collection.csv")
+        sk = step_kernels(path, args.cfg) if os.path.exists(path) else {}
+        if sk:
+            # every launch of a step: the floor of the whole step, not only
+            # of its dominant kernel
+            res["step_kernels_valu"] = sk
+            res["step_valu_wave_instr"] = sum(k["median_per_dispatch"] for k in sk.values())
     if "GRBM_GUI_ACTIVE" in med and durs_all:
         res["clock_ghz_under_pmc"] = med["GRBM_GUI_ACTIVE"] / 8 / statistics.median(durs_all)
     # the kernel build these counters belong to (bench.py ignores counters
