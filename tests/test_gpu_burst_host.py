@@ -356,3 +356,45 @@ def test_host_burst_pinned_layouts(dev, oracle_mod, gap):
                                           nthreads=CPU_THREADS)
     check_decode(got, want, ivlen)
     assert np.array_equal(np.nonzero(got["res"])[0], bad)
+
+
+@pytest.mark.parametrize("memory", ["pageable", "pinned"])
+def test_host_burst_large_datagrams(dev, oracle_mod, memory):
+    """Datagrams up to the UDP maximum (65,507-byte payloads; the reference's
+    receive buffer takes whatever one recvfrom returns, src/sockdgram.c:67-108)
+    mixed with runts and MTU sizes: ~200 MB, so each 64 MiB chunk holds a few
+    thousand datagrams and the burst crosses several chunks in both slots.
+    TX then RX (every 50th datagram tampered) against the oracle."""
+    from ilias_net2_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(8081)
+    n, alg, ivlen = 12001, 6, 16
+    payload = rng.choice(np.array([0, 100, 1428, 9000, 32768, 65507 - 72]), n,
+                         p=[0.05, 0.2, 0.25, 0.2, 0.15, 0.15])
+    lens = (8 + 64 + payload).astype(np.uint32)
+    lens[rng.random(n) < 0.02] = 5                 # runts
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    data = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    seq = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    flags = np.full(n, PH_SIGNED | PH_ENCRYPTED, dtype=np.uint32)
+    key = bytes(range(40, 104))
+    o_res, o_sealed = oracle_mod.packet_encode_batch(
+        alg, key, True, seq, flags, data, offs, lens, nthreads=CPU_THREADS)
+    if memory == "pinned":
+        buf = pinned(data.shape, np.uint8)
+        buf[:] = data
+    else:
+        buf = data.copy()
+    del data
+    res = encode_host(L, alg, key, True, seq, flags, buf, offs, lens)
+    assert np.array_equal(res, o_res)
+    assert np.array_equal(buf, o_sealed)
+    del o_sealed
+    bad = np.nonzero((np.arange(n) % 50 == 7) & (lens > 72))[0]
+    buf[(offs[bad] + 8 + (lens[bad] - 9) // 2).astype(np.int64)] ^= 0x01
+    got = decode_host(L, rx_keys(alg, key, True), ivlen, buf, offs, lens)
+    want = oracle_mod.packet_decode_batch(alg, key, True, ivlen, buf, offs, lens,
+                                          nthreads=CPU_THREADS)
+    check_decode(got, want, ivlen)
+    assert (got["res"][bad] == BAD).all() and (got["res"] == OK).sum() > n // 2
