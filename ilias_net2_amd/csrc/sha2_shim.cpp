@@ -619,11 +619,59 @@ bool d2h_copy()
 }
 
 /*
+ * The byte range [*rs, *re) (offsets from base) of packets off / ln [0, n)
+ * when it can be DMA'd as it lies: within one page-locked allocation (both
+ * ends map to the device at the same distance) and dense -- at most a
+ * quarter more bytes than the packets themselves, as when a receive loop
+ * fills one pinned arena back to back.
+ */
+bool dense_pinned(WorkPool &pool, const uint8_t *base, const uint64_t *off,
+    const uint32_t *ln, uint64_t n, uint64_t *rs, uint64_t *re)
+{
+	const size_t nt = std::min<size_t>(kPackThreads,
+	    std::max<size_t>(1, n >> 14));
+	uint64_t lo_t[kPackThreads], hi_t[kPackThreads], sum_t[kPackThreads];
+	pool.run(nt, [&](size_t t) {
+		uint64_t a = UINT64_MAX, b = 0, m = 0;
+		for (uint64_t j = n * t / nt; j < n * (t + 1) / nt; j++) {
+			a = std::min<uint64_t>(a, off[j]);
+			b = std::max<uint64_t>(b, off[j] + ln[j]);
+			m += ln[j];
+		}
+		lo_t[t] = a;
+		hi_t[t] = b;
+		sum_t[t] = m;
+	});
+	uint64_t a = UINT64_MAX, b = 0, m = 0;
+	for (size_t t = 0; t < nt; t++) {
+		a = std::min(a, lo_t[t]);
+		b = std::max(b, hi_t[t]);
+		m += sum_t[t];
+	}
+	if (n == 0 || b <= a || b - a > m + m / 4)
+		return false;
+	hipPointerAttribute_t pa, pb;
+	if (hipPointerGetAttributes(&pa, base + a) != hipSuccess ||
+	    hipPointerGetAttributes(&pb, base + b - 1) != hipSuccess) {
+		(void)hipGetLastError();
+		return false;
+	}
+	if (pa.type != hipMemoryTypeHost || pb.type != hipMemoryTypeHost ||
+	    (const uint8_t *)pb.devicePointer - (const uint8_t *)pa.devicePointer !=
+	    (ptrdiff_t)(b - 1 - a))
+		return false;
+	*rs = a;
+	*re = b;
+	return true;
+}
+
+/*
  * One chunk [lo, hi) of the caller's packets into slot s: H2D (straight from
- * the caller's buffer when it is pinned and the layout is fixed, else
- * through the slot's pinned staging, packed with 16-byte aligned packet
- * starts), kernel writing the digests to pinned host memory (the caller's
- * buffer when that is pinned).
+ * the caller's buffer when it is pinned -- for the variable layout when the
+ * chunk's packets also lie densely, dense_pinned -- else through the slot's
+ * pinned staging, packed with 16-byte aligned packet starts), kernel
+ * writing the digests to pinned host memory (the caller's buffer when that
+ * is pinned).
  */
 int enqueue_chunk(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
     const uint64_t *offsets, const uint32_t *lens, uint64_t stride,
@@ -636,15 +684,21 @@ int enqueue_chunk(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
 	int rc;
 	PackPlan plan;
 
+	uint64_t rs = 0, re = 0;
+	const bool var_direct = offsets != nullptr && src_pinned &&
+	    dense_pinned(pool, base, offsets + lo, lens + lo, n, &rs, &re);
 	if (offsets == nullptr) {
 		bytes = src_pinned ? (size_t)(n - 1) * stride + fixed_len
 		    : (size_t)n * ((fixed_len + 15) & ~15u);
+	} else if (var_direct) {
+		bytes = re - rs;
 	} else {
 		plan = pack_sizes(pool, lens + lo, n);
 		bytes = plan.start[plan.nt];
 	}
 	const double tr0 = dbg_now();
-	if ((rc = s.reserve(bytes, n, !(offsets == nullptr && src_pinned))) != 0)
+	if ((rc = s.reserve(bytes, n, !((offsets == nullptr && src_pinned) ||
+	    var_direct))) != 0)
 		return rc;
 	if (dbg_timing())
 		fprintf(stderr, "net2: reserve %.3f ms\n", dbg_now() - tr0);
@@ -694,14 +748,34 @@ int enqueue_chunk(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
 		    kout, s.stream));
 	} else {
 		const double tg0 = dbg_now();
-		pack_fill(pool, plan, s.h_in, s.h_off, (uint32_t *)(s.h_off + n),
-		    base, offsets + lo, lens + lo, n);
+		if (var_direct) {
+			/* offsets from the range's start; the bytes as they lie
+			 * (the kernel picks its address mode per wave) */
+			const uint64_t *off = offsets + lo;
+			const uint32_t *ln = lens + lo;
+			uint64_t *ho = s.h_off;
+			uint32_t *hl = (uint32_t *)(s.h_off + n);
+			const size_t nt = std::min<size_t>(kPackThreads,
+			    std::max<size_t>(1, n >> 14));
+			pool.run(nt, [=](size_t t) {
+				for (uint64_t j = n * t / nt; j < n * (t + 1) / nt;
+				    j++) {
+					ho[j] = off[j] - rs;
+					hl[j] = ln[j];
+				}
+			});
+		} else {
+			pack_fill(pool, plan, s.h_in, s.h_off,
+			    (uint32_t *)(s.h_off + n), base, offsets + lo,
+			    lens + lo, n);
+		}
 		if (dbg_timing())
-			fprintf(stderr, "net2: pack %zu B, %llu packets: %.3f ms\n",
-			    bytes, (unsigned long long)n, dbg_now() - tg0);
+			fprintf(stderr, "net2: %s %zu B, %llu packets: %.3f ms\n",
+			    var_direct ? "direct" : "pack", bytes,
+			    (unsigned long long)n, dbg_now() - tg0);
 		if (bytes != 0)
-			HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
-			    hipMemcpyHostToDevice, s.stream));
+			HIP_TRY(hipMemcpyAsync(s.d_in, var_direct ? base + rs :
+			    s.h_in, bytes, hipMemcpyHostToDevice, s.stream));
 		HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, n * 12,
 		    hipMemcpyHostToDevice, s.stream));
 		HIP_TRY(net2_launch_var(alg, s.d_in, s.d_off,
@@ -755,7 +829,9 @@ int run_device_slice(size_t didx, int ordinal, int alg, const uint8_t *base,
 	int rc = 0, cur = 0;
 
 	HIP_TRY(hipSetDevice(ordinal));
-	const bool src_pinned = offsets == nullptr && is_pinned(base);
+	/* fixed layout: DMA'd as it lies; variable: when also dense
+	 * (enqueue_chunk) */
+	const bool src_pinned = is_pinned(base);
 	const bool dst_pinned = is_pinned(digests);
 	/*
 	 * Packets per chunk: kChunkBytes of (padded) payload at the slice's
@@ -1742,53 +1818,12 @@ struct HostBurst {
 	uint8_t *result;
 };
 
-/*
- * The byte range [*rs, *re) (offsets from hb.base) of datagrams [lo, lo + n)
- * when it can be DMA'd as it lies: within one page-locked allocation (both
- * ends map to the device at the same distance) and dense -- at most a
- * quarter more bytes than the datagrams themselves, as when the receive
- * loop fills one pinned arena back to back.
- */
+/* dense_pinned (above) for datagrams [lo, lo + n) of a host burst */
 bool dense_pinned_range(WorkPool &pool, const HostBurst &hb, uint64_t lo,
     uint64_t n, uint64_t *rs, uint64_t *re)
 {
-	const size_t nt = std::min<size_t>(kPackThreads,
-	    std::max<size_t>(1, n >> 14));
-	uint64_t lo_t[kPackThreads], hi_t[kPackThreads], sum_t[kPackThreads];
-	const uint64_t *off = hb.offsets + lo;
-	const uint32_t *ln = hb.lens + lo;
-	pool.run(nt, [&](size_t t) {
-		uint64_t a = UINT64_MAX, b = 0, m = 0;
-		for (uint64_t j = n * t / nt; j < n * (t + 1) / nt; j++) {
-			a = std::min<uint64_t>(a, off[j]);
-			b = std::max<uint64_t>(b, off[j] + ln[j]);
-			m += ln[j];
-		}
-		lo_t[t] = a;
-		hi_t[t] = b;
-		sum_t[t] = m;
-	});
-	uint64_t a = UINT64_MAX, b = 0, m = 0;
-	for (size_t t = 0; t < nt; t++) {
-		a = std::min(a, lo_t[t]);
-		b = std::max(b, hi_t[t]);
-		m += sum_t[t];
-	}
-	if (n == 0 || b <= a || b - a > m + m / 4)
-		return false;
-	hipPointerAttribute_t pa, pb;
-	if (hipPointerGetAttributes(&pa, hb.base + a) != hipSuccess ||
-	    hipPointerGetAttributes(&pb, hb.base + b - 1) != hipSuccess) {
-		(void)hipGetLastError();
-		return false;
-	}
-	if (pa.type != hipMemoryTypeHost || pb.type != hipMemoryTypeHost ||
-	    (const uint8_t *)pb.devicePointer - (const uint8_t *)pa.devicePointer !=
-	    (ptrdiff_t)(b - 1 - a))
-		return false;
-	*rs = a;
-	*re = b;
-	return true;
+	return dense_pinned(pool, hb.base, hb.offsets + lo, hb.lens + lo, n, rs,
+	    re);
 }
 
 /* Chunk [lo, hi) of a host burst into slot s. */

@@ -84,6 +84,37 @@ def test_var_byte_balanced(dev, virtual, oracle_mod, k):
         assert _bad(got, want).size == 0, (alg, _bad(got, want))
 
 
+@pytest.mark.parametrize("k", [1, 3])
+@pytest.mark.parametrize("gap", [0, 5, 3000])
+def test_var_pinned_source(dev, virtual, oracle_mod, k, gap):
+    """Variable layout from page-locked memory: chunks whose packets lie
+    densely in the pinned buffer (gap 0 / 5 bytes, byte-aligned starts) go to
+    the GPU as they lie, a sparse one (3,000-byte gaps) is packed as from
+    pageable memory; pinned and pageable digests destinations; every digest
+    against the oracle, sliced over k devices."""
+    from ilias_net2_amd import _lib
+    virtual(k)
+    lens = synth.mixed_lengths(400 + gap, 60000, choices=(0, 1, 64, 511, 1500, 9000))
+    data, offs = synth.packed(401 + gap, lens, align=1, gap=gap)
+    offs = offs.astype(np.uint64)
+    lens = lens.astype(np.uint32)
+    src = torch.from_numpy(data).pin_memory()
+    for alg in (1, 3):
+        want = oracle_mod.batch(alg, data, offsets=offs, lens=lens,
+                                nthreads=CPU_THREADS)
+        dl = want.shape[1]
+        for pinned_out in (True, False):
+            out = torch.zeros((len(lens), dl), dtype=torch.uint8)
+            if pinned_out:
+                out = out.pin_memory()
+            rc = _lib.lib().net2_sha2_batch(
+                alg, src.data_ptr(), offs.ctypes.data, lens.ctypes.data, 0, 0,
+                len(lens), out.data_ptr(), k)
+            assert rc == 0, rc
+            got = out.numpy()
+            assert _bad(got, want).size == 0, (alg, pinned_out, _bad(got, want))
+
+
 def test_fewer_packets_than_devices(dev, virtual, oracle_mod):
     from ilias_net2_amd import batch
     virtual(8)
