@@ -92,3 +92,42 @@ def test_random_hmac_layouts(dev, oracle_mod, seed):
                          lens=_dev(lens.astype(np.int32), dev),
                          binned=bool(seed % 2)).cpu().numpy()
     assert np.array_equal(got, want), (seed, alg, align, gap)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_sign_verify_layouts(dev, oracle_mod, seed):
+    """The datagram authenticator on random layouts (types/packet.n2t:226-257,
+    410-427): sign in place, tamper with a few datagrams (in the field or the
+    message), verify -- every sealed byte and every verdict against the
+    oracle's HMAC, binned and unbinned, at every start alignment (the SHA-256
+    sign / verify instances take the pair loop since round 5)."""
+    from ilias_net2_amd import batch
+    rng = np.random.default_rng(9000 + seed)
+    lens, align, gap = _layout(rng)
+    alg = int(rng.integers(4, 7))
+    dl = {4: 32, 5: 48, 6: 64}[alg]
+    lens = (lens + np.where(rng.random(len(lens)) < 0.9, dl, 0)).astype(np.uint32)
+    key = bytes(synth.random_bytes(9100 + seed, dl))
+    data, offs = synth.packed(9200 + seed, lens, align=align, gap=gap)
+    sealed = data.copy()
+    for o, l in zip(offs, lens):
+        o, l = int(o), int(l)
+        if l >= dl:
+            sealed[o:o + dl] = np.frombuffer(oracle_mod.hmac(
+                alg, key, data[o + dl:o + l].tobytes()), dtype=np.uint8)
+    binned = bool(seed % 2)
+    d = _dev(data, dev)
+    o_t = _dev(offs.astype(np.int64), dev)
+    l_t = _dev(lens.astype(np.int32), dev)
+    batch.hmac_sign_dev(alg, key, d, o_t, l_t, binned=binned)
+    got = d.cpu().numpy()
+    assert np.array_equal(got, sealed), (seed, alg, align, gap)
+    rx = sealed.copy()
+    want = np.where(lens >= dl, 0, 2).astype(np.uint8)
+    for i in np.nonzero((rng.random(len(lens)) < 0.1) & (lens > 0))[0]:
+        rx[int(offs[i]) + int(rng.integers(0, lens[i]))] ^= 0x08
+        if lens[i] >= dl:
+            want[i] = 1
+    v = batch.hmac_verify_dev(alg, key, _dev(rx, dev), o_t, l_t,
+                              binned=binned).cpu().numpy()
+    assert np.array_equal(v, want), (seed, alg, align, gap, np.nonzero(v != want)[0][:8])
