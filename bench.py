@@ -567,9 +567,21 @@ def rooflines(name, launch_ms, per_launch, sclk_mhz=None):
             "steps at %.0f MHz (> 3 %% apart): counters not joined" % (
                 name, pmc_mhz, sclk_mhz))
         pmc = None
+    box_mhz = ((pmc or {}).get("trace_box") or {}).get("sclk_mhz_during_timed_steps")
+    if pmc and sclk_mhz and box_mhz and abs(box_mhz / sclk_mhz - 1) > 0.03:
+        # the kernel trace committed beside the counters was taken on a box
+        # that timed this config at another clock: its average duration
+        # would not be this line's
+        roof["traffic_note"] = (
+            "profiles/pmc_%s.json's trace box timed this config at %d MHz, "
+            "this line's timed steps ran at %.0f MHz (> 3 %% apart): counters "
+            "not joined" % (name, box_mhz, sclk_mhz))
+        pmc = None
     if pmc:
         roof["counters_clock_mhz"] = round(pmc_mhz) if pmc_mhz else None
         roof["counters_box"] = pmc.get("trace_box")
+        roof["trace_kernel_ms"] = round(pmc["trace_avg_ns"] / 1e6, 4) \
+            if pmc.get("trace_avg_ns") else None
     if pmc:
         roof["traffic"] = pmc.get("hbm_bytes_per_launch")
         roof["traffic_build_id"] = pmc.get("kernel_build_id")
@@ -805,10 +817,76 @@ def main():
         if rank == 0:
             line["cpu_baseline"] = cb
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        print(json.dumps(finalize_line(line)), flush=True)
     if ws > 1:
         dist.destroy_process_group()
     return None
+
+
+# Strings kept where they are when a line is finalized; any other string
+# over NOTE_MIN characters moves to the line's "notes" (finalize_line).
+KEEP_PROSE = {("metric",), ("unit",), ("data",), ("config", "workload"),
+              ("config", "parallelism"), ("cpu_baseline", "sample"),
+              ("cpu_baseline", "unit"), ("cpu_baseline", "kind")}
+NOTE_MIN = 60
+
+
+def _hoist(obj, path, notes):
+    for k in list(obj):
+        v, p = obj[k], path + (k,)
+        if isinstance(v, dict):
+            _hoist(v, p, notes)
+        elif isinstance(v, str) and len(v) > NOTE_MIN and p not in KEEP_PROSE:
+            notes[".".join(p)] = v
+            del obj[k]
+
+
+def _brief(r):
+    """The numbers of one config for the line's closing summary."""
+    if not isinstance(r, dict):
+        return None
+    out = {k: r[k] for k in ("value", "ms_per_step") if k in r}
+    roof = r.get("roofline") or {}
+    for k, kk in (("kernel_ms", "kernel_ms"), ("frac", "frac"),
+                  ("traffic_over_algorithmic", "traffic_x")):
+        if roof.get(k) is not None:
+            out[kk] = roof[k]
+    if isinstance(r.get("pageable"), dict):
+        out["pageable_value"] = r["pageable"].get("value")
+    cb = r.get("cpu_baseline")
+    if isinstance(cb, dict) and cb.get("value"):
+        out["cpu_value"] = round(cb["value"], 1)
+    return out
+
+
+def finalize_line(line):
+    """The printed form of a line: long prose moved into one "notes" object
+    near the front, and every config's numbers repeated in a short
+    "summary" that closes the line, so a reader of only its last ~2 KB (the
+    driver's record keeps a tail) still has C2, C3, C4 and the end-to-end
+    rates."""
+    notes = {}
+    body = dict(line)
+    for k in list(body):
+        if isinstance(body[k], dict):
+            _hoist(body[k], (k,), notes)
+    front = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+             "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")
+    out = {k: body.pop(k) for k in front if k in body}
+    if notes:
+        out["notes"] = notes
+    out.update(body)
+    summary = {"line": _brief(line)}
+    for k, r in (line.get("extra_configs") or {}).items():
+        b = _brief(r)
+        if k == "c1" and isinstance(r, dict):
+            st = r.get("stages", {})
+            b = {s: st[s].get("ms") for s in ("gpu_digest_sha512", "cpu_digest_sha512_1core",
+                                               "sc_hash_tick") if s in st}
+        if b:
+            summary[k] = b
+    out["summary"] = summary
+    return out
 
 
 def extra_configs(args, dev, probe, ws=1, rank=0, label=None):

@@ -13,7 +13,9 @@ import os
 LIB_NAME = "libnet2_sha2.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # Build-variant A/B runs (tools/gpu_ab_lib.sh) point this at another build of
-# the same library; unset, the in-tree library is the one loaded.
+# the same library; unset, the in-tree library is the one loaded.  A build
+# lacking an entry point of this ABI is refused unless
+# NET2_SHA2_LIB_ALLOW_OLD_ABI=1 (bind()).
 LIB_PATH = os.environ.get("NET2_SHA2_LIB", LIB_PATH)
 
 # Registry rows (include/net2/sha2_batch.h, include/net2/hash.h).
@@ -59,6 +61,8 @@ SIGNATURES = {
     "net2_sha2_numa_stats": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_void_p]),
     "net2_sha2_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "net2_sha2_set_device": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+    "net2_sha2_get_device": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "net2_sha2_last_hip_error": (ctypes.c_int, []),
     "net2_sha2_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "net2_sha2_dev_fixed": (ctypes.c_int, [
@@ -178,15 +182,33 @@ def lib() -> ctypes.CDLL:
                 "`python -c 'import __graft_entry__ as g; g.build()'` "
                 "(there is no CPU fallback for the SHA-2 path)")
         _share_torch_hip_runtime()
-        handle = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in SIGNATURES.items():
-            if "NET2_SHA2_LIB" in os.environ and not hasattr(handle, name):
-                continue    # an A/B build of an earlier round: older ABI
-            fn = getattr(handle, name)
-            fn.restype = res
-            fn.argtypes = args
-        _lib = handle
+        _lib = bind(ctypes.CDLL(LIB_PATH),
+                    allow_old_abi=os.environ.get("NET2_SHA2_LIB_ALLOW_OLD_ABI") == "1")
     return _lib
+
+
+def bind(handle: ctypes.CDLL, allow_old_abi: bool = False) -> ctypes.CDLL:
+    """Declare every SIGNATURES entry on a loaded build of the library.
+
+    A missing symbol raises, naming every one missing, unless allow_old_abi
+    (NET2_SHA2_LIB_ALLOW_OLD_ABI=1: an A/B build of an earlier round, whose
+    ABI may lack later entry points; the names skipped are logged)."""
+    missing = [name for name in SIGNATURES if not hasattr(handle, name)]
+    if missing and not allow_old_abi:
+        raise ImportError(f"{handle._name} lacks {len(missing)} entry point(s) of "
+                          f"this ABI: {', '.join(missing)} (an older build? set "
+                          "NET2_SHA2_LIB_ALLOW_OLD_ABI=1 for A/B runs)")
+    if missing:
+        import sys
+        print(f"_lib: {handle._name}: older ABI, not bound: {', '.join(missing)}",
+              file=sys.stderr, flush=True)
+    for name, (res, args) in SIGNATURES.items():
+        if name in missing:
+            continue
+        fn = getattr(handle, name)
+        fn.restype = res
+        fn.argtypes = args
+    return handle
 
 
 def strerror(rc: int) -> str:

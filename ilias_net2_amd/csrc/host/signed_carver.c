@@ -74,6 +74,7 @@ struct sc_task {
 	void		*(*fn)(void *);
 	void		*arg;
 	struct sc_batch	*b;
+	int		 dev;		/* the submitter's device index */
 };
 
 static struct {
@@ -97,12 +98,28 @@ pool_pop(struct sc_task *t)
 	return 1;
 }
 
-/* run t outside the lock, then count it done (lock held on entry/exit) */
+/*
+ * run t outside the lock, then count it done (lock held on entry/exit).  The
+ * task runs on its submitter's GPU (net2_sha2_set_device): a helper thread
+ * has no device of its own, and one that helps another tick must not hash
+ * that tick's payloads on its own device.
+ */
 static void
 pool_run(struct sc_task *t)
 {
+	int own = -1, prev = -1, set = 0;
+
 	pthread_mutex_unlock(&g_pool.mu);
+	if (t->dev >= 0 && net2_sha2_get_device(&own) == 0 && own != t->dev)
+		set = net2_sha2_set_device(t->dev, &prev) == 0;
 	t->fn(t->arg);
+	if (set) {
+		/* back to this thread's own device (and its HIP device: the
+		 * selection moved it), then to its own selection */
+		(void)net2_sha2_set_device(prev >= 0 ? prev : own, NULL);
+		if (prev < 0)
+			(void)net2_sha2_set_device(-1, NULL);
+	}
 	pthread_mutex_lock(&g_pool.mu);
 	if (--t->b->left == 0)
 		pthread_cond_broadcast(&t->b->done);
@@ -134,6 +151,7 @@ pool_run_batch(void *(*fn)(void *), void **args, size_t n, int nthreads)
 	struct sc_batch b;
 	struct sc_task t;
 	size_t k;
+	int dev = -1;
 
 	if (n == 0)
 		return;
@@ -143,6 +161,8 @@ pool_run_batch(void *(*fn)(void *), void **args, size_t n, int nthreads)
 		return;
 	}
 	b.left = n - 1;
+	if (net2_sha2_get_device(&dev) != 0)
+		dev = -1;
 	pthread_cond_init(&b.done, NULL);
 	pthread_mutex_lock(&g_pool.mu);
 	/* room for this batch's tasks on the ring */
@@ -175,7 +195,7 @@ pool_run_batch(void *(*fn)(void *), void **args, size_t n, int nthreads)
 	}
 	for (k = 1; k < n; k++) {
 		g_pool.q[(g_pool.qhead + g_pool.qlen) % g_pool.qcap] =
-		    (struct sc_task){ fn, args[k], &b };
+		    (struct sc_task){ fn, args[k], &b, dev };
 		g_pool.qlen++;
 	}
 	pthread_cond_broadcast(&g_pool.work);

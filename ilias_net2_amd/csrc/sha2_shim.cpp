@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <deque>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -56,6 +57,55 @@ int hip_fail(hipError_t e)
 		if (_e != hipSuccess)                                        \
 			return hip_fail(_e);                                 \
 	} while (0)
+
+/*
+ * Test-only fault injection (a -DNET2_FAULT_INJECT=1 build, libnet2_sha2_fi.so;
+ * the shipped library compiles it out).  net2_fault_inject(site, k) makes the
+ * k-th pass through `site` of a host-pipeline chunk fail as if its HIP call
+ * had: FI_H2D once the chunk's input copy is queued, FI_KERNEL once its first
+ * kernel is launched, FI_RECORD in place of the chunk's event record.
+ * tests/test_gpu_failures.py drives it.
+ */
+#ifndef NET2_FAULT_INJECT
+#define NET2_FAULT_INJECT 0
+#endif
+enum { FI_H2D = 1, FI_KERNEL = 2, FI_RECORD = 3 };
+#if NET2_FAULT_INJECT
+std::atomic<int> g_fi_site{0}, g_fi_left{0};
+bool fi_hit(int site)
+{
+	if (g_fi_site.load(std::memory_order_relaxed) != site)
+		return false;
+	if (g_fi_left.fetch_sub(1, std::memory_order_relaxed) != 1)
+		return false;
+	g_fi_site.store(0, std::memory_order_relaxed);
+	return true;
+}
+#else
+constexpr bool fi_hit(int) { return false; }
+#endif
+#define FI_POINT(site)                                                       \
+	do {                                                                 \
+		if (fi_hit(site))                                            \
+			return hip_fail(hipErrorLaunchFailure);              \
+	} while (0)
+
+/*
+ * After a chunk failed part-way: wait for whatever it already queued on its
+ * stream (a copy still reading the caller's input or the slot's staging, a
+ * kernel still storing into the caller's mapped output), so nothing of the
+ * failed call runs after it returns and the slot can be reused.  The first
+ * error's HIP code is kept for net2_sha2_last_hip_error.
+ */
+void quiesce(hipStream_t st)
+{
+	if (st == nullptr)
+		return;
+	const int keep = tl_last_hip_error;
+	(void)hipStreamSynchronize(st);
+	(void)hipGetLastError();
+	tl_last_hip_error = keep;
+}
 
 /* ---- registry (include/net2/hash.h) ------------------------------------ */
 
@@ -250,7 +300,10 @@ struct Slot {
  * sooner), then sleep on a condition variable.  The job word packs the
  * generation with nt, so a worker that wakes late never runs a job it is
  * not counted in.  Pools are never destroyed (their threads are detached
- * and may be parked at process exit).
+ * and may be parked at process exit).  One job at a time: job_, pending_
+ * and word_ describe a single job, so run() is serialised by run_mu_ -- a
+ * device's pool is shared by net2_sha2_batch and the host packet bursts,
+ * which hold different locks and may run at once on one device.
  */
 #ifndef NET2_POOL_SPIN_US
 #define NET2_POOL_SPIN_US 500
@@ -265,6 +318,7 @@ public:
 			f((size_t)0);
 			return;
 		}
+		std::lock_guard<std::mutex> one(run_mu_);
 		grow(nt - 1);
 		const std::function<void(size_t)> job = f;
 		job_ = &job;
@@ -331,6 +385,7 @@ private:
 	std::atomic<size_t> pending_{0};
 	const std::function<void(size_t)> *job_ = nullptr;
 	size_t nworkers_ = 0;
+	std::mutex run_mu_;	/* one run() at a time */
 	std::mutex m_;
 	std::condition_variable cv_;
 };
@@ -520,6 +575,44 @@ bool is_pinned(const void *p)
 	return a.type == hipMemoryTypeHost;
 }
 
+/*
+ * [p, p + bytes) lies in one page-locked allocation, so the GPU may DMA from
+ * it or store into it through its device mapping: both ends are page-locked,
+ * map to the device at the same distance as on the host, and belong to the
+ * same allocation (the same HIP buffer id).
+ * A range that only starts in a registered region -- or spans two adjacent
+ * page-locked allocations -- fails, and the caller stages it instead.
+ */
+bool pinned_span(const void *p, size_t bytes)
+{
+	if (p == nullptr || bytes == 0)
+		return false;
+	const uint8_t *a = (const uint8_t *)p, *b = a + bytes - 1;
+	hipPointerAttribute_t pa, pb;
+	if (hipPointerGetAttributes(&pa, a) != hipSuccess ||
+	    hipPointerGetAttributes(&pb, b) != hipSuccess) {
+		(void)hipGetLastError();
+		return false;
+	}
+	if (pa.type != hipMemoryTypeHost || pb.type != hipMemoryTypeHost ||
+	    pa.devicePointer == nullptr ||
+	    (const uint8_t *)pb.devicePointer - (const uint8_t *)pa.devicePointer !=
+	    (ptrdiff_t)(bytes - 1))
+		return false;
+	/* hipMemGetAddressRange reports no base for hipHostRegister'ed memory
+	 * on this runtime; the buffer id names the allocation for both kinds
+	 * (tools/ptr_probe.py, profiles/round6/ptr_probe.txt) */
+	unsigned long long ida = 0, idb = 0;
+	if (hipPointerGetAttribute(&ida, HIP_POINTER_ATTRIBUTE_BUFFER_ID,
+	    (hipDeviceptr_t)a) != hipSuccess ||
+	    hipPointerGetAttribute(&idb, HIP_POINTER_ATTRIBUTE_BUFFER_ID,
+	    (hipDeviceptr_t)b) != hipSuccess) {
+		(void)hipGetLastError();
+		return false;
+	}
+	return ida == idb && ida != 0;
+}
+
 /* memcpy of a large range split over the pool's threads (staging copies). */
 void par_memcpy(WorkPool &pool, uint8_t *dst, const uint8_t *src,
     size_t bytes)
@@ -620,8 +713,8 @@ bool d2h_copy()
 
 /*
  * The byte range [*rs, *re) (offsets from base) of packets off / ln [0, n)
- * when it can be DMA'd as it lies: within one page-locked allocation (both
- * ends map to the device at the same distance) and dense -- at most a
+ * when it can be DMA'd as it lies: within one page-locked allocation
+ * (pinned_span) and dense -- at most a
  * quarter more bytes than the packets themselves, as when a receive loop
  * fills one pinned arena back to back.
  */
@@ -648,17 +741,7 @@ bool dense_pinned(WorkPool &pool, const uint8_t *base, const uint64_t *off,
 		b = std::max(b, hi_t[t]);
 		m += sum_t[t];
 	}
-	if (n == 0 || b <= a || b - a > m + m / 4)
-		return false;
-	hipPointerAttribute_t pa, pb;
-	if (hipPointerGetAttributes(&pa, base + a) != hipSuccess ||
-	    hipPointerGetAttributes(&pb, base + b - 1) != hipSuccess) {
-		(void)hipGetLastError();
-		return false;
-	}
-	if (pa.type != hipMemoryTypeHost || pb.type != hipMemoryTypeHost ||
-	    (const uint8_t *)pb.devicePointer - (const uint8_t *)pa.devicePointer !=
-	    (ptrdiff_t)(b - 1 - a))
+	if (n == 0 || b <= a || b - a > m + m / 4 || !pinned_span(base + a, b - a))
 		return false;
 	*rs = a;
 	*re = b;
@@ -673,7 +756,7 @@ bool dense_pinned(WorkPool &pool, const uint8_t *base, const uint64_t *off,
  * writing the digests to pinned host memory (the caller's buffer when that
  * is pinned).
  */
-int enqueue_chunk(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
+int enqueue_chunk_steps(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
     const uint64_t *offsets, const uint32_t *lens, uint64_t stride,
     uint32_t fixed_len, uint64_t lo, uint64_t hi, uint8_t *user_dig,
     bool src_pinned, bool dst_pinned)
@@ -721,8 +804,10 @@ int enqueue_chunk(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
 		if (bytes != 0)
 			HIP_TRY(hipMemcpyAsync(s.d_in, base + lo * stride,
 			    bytes, hipMemcpyHostToDevice, s.stream));
+		FI_POINT(FI_H2D);
 		HIP_TRY(net2_launch_fixed(alg, s.d_in, stride, fixed_len, n,
 		    kout, s.stream));
+		FI_POINT(FI_KERNEL);
 	} else if (offsets == nullptr) {
 		const size_t st = (fixed_len + 15) & ~15u;
 		if (st == stride) {
@@ -744,8 +829,10 @@ int enqueue_chunk(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
 		if (bytes != 0)
 			HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
 			    hipMemcpyHostToDevice, s.stream));
+		FI_POINT(FI_H2D);
 		HIP_TRY(net2_launch_fixed(alg, s.d_in, st, fixed_len, n,
 		    kout, s.stream));
+		FI_POINT(FI_KERNEL);
 	} else {
 		const double tg0 = dbg_now();
 		if (var_direct) {
@@ -778,18 +865,35 @@ int enqueue_chunk(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
 			    s.h_in, bytes, hipMemcpyHostToDevice, s.stream));
 		HIP_TRY(hipMemcpyAsync(s.d_off, s.h_off, n * 12,
 		    hipMemcpyHostToDevice, s.stream));
+		FI_POINT(FI_H2D);
 		HIP_TRY(net2_launch_var(alg, s.d_in, s.d_off,
 		    (const uint32_t *)(s.d_off + n), n, kout,
 		    n >= 4096 ? s.d_ws : nullptr, s.stream));
+		FI_POINT(FI_KERNEL);
 	}
 	if (!direct)
 		HIP_TRY(hipMemcpyAsync(host_dig, s.d_dig, (size_t)n * dl,
 		    hipMemcpyDeviceToHost, s.stream));
+	FI_POINT(FI_RECORD);
 	HIP_TRY(hipEventRecord(s.done, s.stream));
 	s.busy = true;
 	s.user_dig = dst_pinned ? nullptr : user_dig;
 	s.user_bytes = (size_t)n * dl;
 	return 0;
+}
+
+/* enqueue_chunk_steps; a chunk that fails part-way is waited for (quiesce)
+ * before the error goes back, and its slot stays free. */
+int enqueue_chunk(WorkPool &pool, Slot &s, int alg, const uint8_t *base,
+    const uint64_t *offsets, const uint32_t *lens, uint64_t stride,
+    uint32_t fixed_len, uint64_t lo, uint64_t hi, uint8_t *user_dig,
+    bool src_pinned, bool dst_pinned)
+{
+	const int rc = enqueue_chunk_steps(pool, s, alg, base, offsets, lens,
+	    stride, fixed_len, lo, hi, user_dig, src_pinned, dst_pinned);
+	if (rc != 0)
+		quiesce(s.stream);
+	return rc;
 }
 
 int drain(Slot &s)
@@ -829,10 +933,16 @@ int run_device_slice(size_t didx, int ordinal, int alg, const uint8_t *base,
 	int rc = 0, cur = 0;
 
 	HIP_TRY(hipSetDevice(ordinal));
-	/* fixed layout: DMA'd as it lies; variable: when also dense
-	 * (enqueue_chunk) */
-	const bool src_pinned = is_pinned(base);
-	const bool dst_pinned = is_pinned(digests);
+	/* fixed layout: DMA'd as it lies when the slice's whole span is in one
+	 * page-locked allocation; variable: when its chunk's packets also lie
+	 * densely in one (enqueue_chunk, dense_pinned).  Digests are stored
+	 * through the output's mapping only when the slice's whole output range
+	 * is in one page-locked allocation (pinned_span). */
+	const bool src_pinned = offsets == nullptr ?
+	    pinned_span(base + lo * stride, (size_t)(hi - 1 - lo) * stride +
+	    fixed_len) : is_pinned(base);
+	const bool dst_pinned = pinned_span(digests + lo * dl,
+	    (size_t)(hi - lo) * dl);
 	/*
 	 * Packets per chunk: kChunkBytes of (padded) payload at the slice's
 	 * mean packet size.  A chunk of unusually large packets just grows the
@@ -876,11 +986,21 @@ int run_device_slice(size_t didx, int ordinal, int alg, const uint8_t *base,
 	return rc ? rc : rc2 ? rc2 : rc3;
 }
 
-/* The device a single-message call runs on: the calling thread's current
- * device when it is a usable one (one process per GPU stays on its GPU),
- * else the first. */
+/*
+ * The calling thread's device selection (net2_sha2_set_device): an index
+ * into the device list (batch_devices()), or -1 to follow the thread's
+ * current HIP device.  Helper threads that run work submitted by another
+ * thread (the signed carver's pool) take the submitter's selection.
+ */
+thread_local int tl_dev_sel = -1;
+
+/* The device (index into dv = batch_devices()) a single-message call runs
+ * on: the thread's selection; else its current HIP device when that is a
+ * usable one (one process per GPU stays on its GPU); else the first. */
 size_t small_device(const std::vector<int> &dv)
 {
+	if (tl_dev_sel >= 0 && (size_t)tl_dev_sel < dv.size())
+		return (size_t)tl_dev_sel;
 	int cur = -1;
 	(void)hipGetDevice(&cur);
 	for (size_t d = 0; d < dv.size(); d++)
@@ -890,12 +1010,66 @@ size_t small_device(const std::vector<int> &dv)
 }
 
 /*
+ * One persistent host thread per device index for the slices of a sharded
+ * call (shard_batch): a thread created and joined per call cost ~30-60 us
+ * per extra device on every net2_sha2_batch / host burst.  Jobs of
+ * concurrent callers queue in order; a slice takes its device's lock anyway.
+ * Workers are detached and live as long as the process.
+ */
+class SliceWorker {
+public:
+	void post(std::function<void()> f)
+	{
+		std::lock_guard<std::mutex> g(m_);
+		if (!started_) {
+			std::thread([this]() { loop(); }).detach();
+			started_ = true;
+		}
+		q_.push_back(std::move(f));
+		cv_.notify_one();
+	}
+
+private:
+	void loop()
+	{
+		for (;;) {
+			std::function<void()> f;
+			{
+				std::unique_lock<std::mutex> lk(m_);
+				cv_.wait(lk, [&]() { return !q_.empty(); });
+				f = std::move(q_.front());
+				q_.pop_front();
+			}
+			f();
+		}
+	}
+
+	std::mutex m_;
+	std::condition_variable cv_;
+	std::deque<std::function<void()>> q_;
+	bool started_ = false;
+};
+
+SliceWorker *slice_worker(size_t idx)
+{
+	static std::mutex mu;
+	static std::vector<SliceWorker *> w;	/* never freed, see above */
+	std::lock_guard<std::mutex> g(mu);
+	if (w.size() <= idx)
+		w.resize(idx + 1, nullptr);
+	if (w[idx] == nullptr)
+		w[idx] = new SliceWorker();
+	return w[idx];
+}
+
+/*
  * Shards a host-memory batch of n packets over the devices (net2_sha2_batch,
  * the host packet bursts): contiguous slices -- by packet count for the
  * fixed layout (lens == NULL), by bytes otherwise -- no slice under
- * slice_min_bytes() of payload, one host thread per extra device.  The
- * device list starts at the caller's current device, so one process per GPU
- * with max_devices == 1 stays on its own device.  fn(didx, ordinal, lo, hi)
+ * slice_min_bytes() of payload, each extra device's slice on that device's
+ * persistent worker (SliceWorker).  The device list starts at the caller's
+ * device (small_device), so one process per GPU with max_devices == 1 stays
+ * on its own device.  fn(didx, ordinal, lo, hi)
  * runs one slice; the first error is returned.
  */
 template <class F>
@@ -942,20 +1116,28 @@ int shard_batch(uint64_t n, const uint32_t *lens, uint32_t fixed_len,
 
 	int prev = -1;
 	(void)hipGetDevice(&prev);
-	size_t first = 0;
-	for (size_t d = 0; d < dv.size(); d++)
-		if (dv[d] == prev)
-			first = d;
+	const size_t first = small_device(dv);
 	std::vector<int> rcs(nd, 0);
-	std::vector<std::thread> th;
-	for (size_t d = 1; d < nd; d++)
-		th.emplace_back([&, d]() {
-			const size_t e = (first + d) % dv.size();
+	struct {
+		std::mutex m;
+		std::condition_variable cv;
+		size_t left;
+	} done;
+	done.left = nd - 1;
+	for (size_t d = 1; d < nd; d++) {
+		const size_t e = (first + d) % dv.size();
+		slice_worker(e)->post([&, d, e]() {
 			rcs[d] = fn(e, dv[e], cut[d], cut[d + 1]);
+			std::lock_guard<std::mutex> g(done.m);
+			if (--done.left == 0)
+				done.cv.notify_all();
 		});
+	}
 	rcs[0] = fn(first, dv[first], cut[0], cut[1]);
-	for (std::thread &t : th)
-		t.join();
+	{
+		std::unique_lock<std::mutex> lk(done.m);
+		done.cv.wait(lk, [&]() { return done.left == 0; });
+	}
 	if (prev >= 0)
 		(void)hipSetDevice(prev);
 	for (int r : rcs)
@@ -968,7 +1150,7 @@ int shard_batch(uint64_t n, const uint32_t *lens, uint32_t fixed_len,
 
 int net2_co_run(const net2co::Request &r)
 {
-	const std::vector<int> &dv = devices();
+	const std::vector<int> dv = batch_devices();
 	if (dv.empty())
 		return ENODEV;
 	const size_t d = small_device(dv);
@@ -984,7 +1166,7 @@ int net2_co_run(const net2co::Request &r)
 NET2_EXPORT int net2_coalesce_stats(int device, uint64_t *calls,
     uint64_t *launches)
 {
-	const std::vector<int> &dv = devices();
+	const std::vector<int> dv = batch_devices();
 	if (dv.empty())
 		return ENODEV;
 	if (device < -1 || device >= (int)dv.size())
@@ -1008,6 +1190,47 @@ NET2_EXPORT int net2_sha2_device_count(int *count)
 	*count = (int)devices().size();
 	return *count > 0 ? 0 : ENODEV;
 }
+
+NET2_EXPORT int net2_sha2_set_device(int index, int *prev)
+{
+	if (prev != nullptr)
+		*prev = tl_dev_sel;
+	if (index == -1) {
+		tl_dev_sel = -1;
+		return 0;
+	}
+	const std::vector<int> dv = batch_devices();
+	if (dv.empty())
+		return ENODEV;
+	if (index < -1 || index >= (int)dv.size())
+		return EINVAL;
+	HIP_TRY(hipSetDevice(dv[index]));
+	tl_dev_sel = index;
+	return 0;
+}
+
+NET2_EXPORT int net2_sha2_get_device(int *index)
+{
+	if (index == nullptr)
+		return EINVAL;
+	const std::vector<int> dv = batch_devices();
+	if (dv.empty())
+		return ENODEV;
+	*index = (int)small_device(dv);
+	return 0;
+}
+
+#if NET2_FAULT_INJECT
+NET2_EXPORT int net2_fault_inject(int site, int k)
+{
+	if (site < 0 || site > FI_RECORD || k < 0)
+		return EINVAL;
+	g_fi_site.store(0);
+	g_fi_left.store(k);
+	g_fi_site.store(k > 0 ? site : 0);
+	return 0;
+}
+#endif
 
 NET2_EXPORT int net2_sha2_last_hip_error(void)
 {
@@ -1496,6 +1719,23 @@ int check_burst_args(int hash_alg, const void *key, size_t keylen,
 }
 
 /*
+ * The binning workspace a burst's HMAC kernel is given: below
+ * NET2_BURST_BIN_MIN datagrams (default 4,096, as net2_sha2_batch's
+ * host path) none -- the batch is a few waves on an otherwise idle chip,
+ * its time is its longest wave's whatever the order, and the binning
+ * launch is pure fixed cost (tools/burst_sizes.py).
+ */
+uint32_t *burst_bins(uint64_t n, uint32_t *bin)
+{
+	static const uint64_t min_n = []() {
+		const char *e = getenv("NET2_BURST_BIN_MIN");
+		return e != nullptr && *e != '\0' ? strtoull(e, nullptr, 10) :
+		    (uint64_t)4096;
+	}();
+	return n >= min_n ? bin : nullptr;
+}
+
+/*
  * The hash steps of net2_packet_decode for a device-resident burst.
  * hdr_out: d_seq / d_flags are copies the final kernel makes (the host
  * path: mapped host memory) -- the HMAC kernel keeps the decoded headers in
@@ -1534,12 +1774,14 @@ int decode_burst(const struct net2_burst_rx_keys *k, uint32_t ivlen,
 		}
 		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)k->hash_key,
 		    k->hash_keylen, (const uint8_t *)d_base, d_offsets, d_lens, 0,
-		    0, n, w.verdict, w.bin, s, NET2_HMAC_MODE_BURST_RX, &rx));
+		    0, n, w.verdict, burst_bins(n, w.bin), s,
+		    NET2_HMAC_MODE_BURST_RX, &rx));
 	} else {
 		HIP_TRY(net2_launch_burst_prep((uint8_t *)d_base, d_offsets,
 		    d_lens, n, 0, 0, enc_set, 0, nullptr, nullptr, seq,
 		    flags, w.sub_off, w.sub_len, w.status, s));
 	}
+	FI_POINT(FI_KERNEL);
 	HIP_TRY(net2_launch_burst_final(n, w.status, w.verdict, seq, flags,
 	    enc_set ? ivlen : 0, (uint8_t *)d_iv, d_result, s,
 	    hdr_out ? d_seq : nullptr, hdr_out ? d_flags : nullptr));
@@ -1570,13 +1812,15 @@ int encode_burst(int hash_alg, const void *hash_key, size_t hash_keylen,
 		tx.rec = rec;
 		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)hash_key,
 		    hash_keylen, (const uint8_t *)d_base, d_offsets, d_lens, 0,
-		    0, n, (uint8_t *)d_base, w.bin, s, NET2_HMAC_MODE_BURST_TX,
-		    &tx));
+		    0, n, (uint8_t *)d_base, burst_bins(n, w.bin), s,
+		    NET2_HMAC_MODE_BURST_TX, &tx));
+		FI_POINT(FI_KERNEL);
 		return 0;
 	}
 	HIP_TRY(net2_launch_burst_prep((uint8_t *)d_base, d_offsets,
 	    d_lens, n, 1, 0, enc_alg != 0, 0, d_seq, d_flags, nullptr,
 	    nullptr, w.sub_off, w.sub_len, w.status, s));
+	FI_POINT(FI_KERNEL);
 	HIP_TRY(net2_launch_burst_final(n, w.status, nullptr, d_seq, d_flags, 0,
 	    nullptr, d_result, s));
 	return 0;
@@ -1827,7 +2071,7 @@ bool dense_pinned_range(WorkPool &pool, const HostBurst &hb, uint64_t lo,
 }
 
 /* Chunk [lo, hi) of a host burst into slot s. */
-int enqueue_burst_chunk(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
+int enqueue_burst_steps(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
     const BurstPins &pins, uint64_t lo, uint64_t hi)
 {
 	const uint64_t n = hi - lo;
@@ -1881,6 +2125,7 @@ int enqueue_burst_chunk(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 	/* offsets, lengths (and TX headers): one copy */
 	HIP_TRY(hipMemcpyAsync(s.d_meta, s.h_meta,
 	    BurstSlot::meta_bytes(n, hb.tx), hipMemcpyHostToDevice, s.stream));
+	FI_POINT(FI_H2D);
 
 	/* staged results: [code n][IV n x ivlen | records][seq n][flags n] */
 	uint8_t *st_res = s.h_out;
@@ -1931,6 +2176,7 @@ int enqueue_burst_chunk(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 		    k_res, s.d_ws, s.stream, (uint8_t *)recd)) != 0)
 			return rc;
 	}
+	FI_POINT(FI_RECORD);
 	HIP_TRY(hipEventRecord(s.done, s.stream));
 	s.busy = true;
 	const bool tx = hb.tx;
@@ -1981,6 +2227,17 @@ int enqueue_burst_chunk(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 	return 0;
 }
 
+/* enqueue_burst_steps; a chunk that fails part-way is waited for (quiesce)
+ * before the error goes back, and its slot stays free. */
+int enqueue_burst_chunk(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
+    const BurstPins &pins, uint64_t lo, uint64_t hi)
+{
+	const int rc = enqueue_burst_steps(pool, s, hb, pins, lo, hi);
+	if (rc != 0)
+		quiesce(s.stream);
+	return rc;
+}
+
 /* One device's share [lo, hi) of a host burst, chunked and double-buffered. */
 int run_burst_slice(size_t didx, int ordinal, const HostBurst &hb,
     uint64_t lo, uint64_t hi)
@@ -1991,13 +2248,20 @@ int run_burst_slice(size_t didx, int ordinal, const HostBurst &hb,
 	BurstCtx *b = bctx_for(didx);
 	std::lock_guard<std::mutex> g(b->mu);
 	HIP_TRY(hipSetDevice(ordinal));
+	/* outputs are stored through their mapping only when the slice's
+	 * whole range of each is in one page-locked allocation */
+	const uint64_t m = hi - lo;
 	BurstPins pins;
 	pins.base = is_pinned(hb.base);
-	pins.result = is_pinned(hb.result);
+	pins.result = pinned_span(hb.result + lo, m);
 	if (!hb.tx) {
-		pins.iv = hb.iv != nullptr && is_pinned(hb.iv);
-		pins.seq = hb.seq_out != nullptr && is_pinned(hb.seq_out);
-		pins.flags = hb.flags_out != nullptr && is_pinned(hb.flags_out);
+		const uint32_t ivl = hb.keys->enc_alg != 0 ? hb.ivlen : 0;
+		pins.iv = hb.iv != nullptr && ivl > 0 && pinned_span((uint8_t *)hb.iv +
+		    lo * ivl, m * ivl);
+		pins.seq = hb.seq_out != nullptr && pinned_span(hb.seq_out + lo,
+		    m * 4);
+		pins.flags = hb.flags_out != nullptr && pinned_span(hb.flags_out +
+		    lo, m * 4);
 	}
 	const PackPlan all = pack_sizes(*c->pool, hb.lens + lo, hi - lo);
 	const size_t mean = std::max<size_t>(all.start[all.nt] /

@@ -62,6 +62,30 @@ const char *net2_sha2_build_id(void);
 int net2_sha2_device_count(int *count);
 
 /*
+ * The calling thread's device for the single-message calls (net2/hash.h
+ * net2_hashctx_hashiov, the SHA2_CTX calls of net2/sha2.h) and the first
+ * device of its batches: index < the device count (the device list; under
+ * the test knob NET2_SHA2_VIRTUAL_DEVICES=k every GPU is listed k times), or
+ * -1 to follow the thread's current HIP device (the default; a thread whose
+ * current device is not a gfx950 uses the first).  A selection also makes
+ * that GPU the thread's current HIP device.  *prev (may be NULL) receives
+ * the previous selection (-1: none), so a helper thread can run one task on
+ * its submitter's device and restore its own.  0, EINVAL or ENODEV.
+ *
+ * The reference runs signature work on workq threads of a shared
+ * threadpool (include/ilias/net2/threadpool.h:33-34), which have no device
+ * of their own: a caller that drives GPU k hands its selection
+ * (net2_sha2_get_device) to the tasks it submits, as the signed carver's
+ * helper pool does (csrc/host/signed_carver.c pool_run).
+ */
+int net2_sha2_set_device(int index, int *prev);
+
+/* The device index the calling thread's single-message calls go to now
+ * (its selection, else the one its current HIP device maps to).  0, EINVAL
+ * or ENODEV. */
+int net2_sha2_get_device(int *index);
+
+/*
  * NUMA placement of net2_sha2_batch's host-side work (diagnostics): for
  * device index `device` of its device list, the NUMA node the GPU hangs
  * off (-1 when the host does not say), the slices it has run, and how many

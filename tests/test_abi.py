@@ -179,6 +179,29 @@ def test_no_device_fails_loudly():
     aligned = (ctypes.addressof(big) + 7) & ~7
     assert L.net2_sha2_workspace_stats(aligned, L.net2_sha2_dev_var_workspace(0),
                                        ctypes.byref(st)) == errno.ENODEV
+    # the thread's device selection: clearing it is host state and reports
+    # the previous one; selecting a device needs one
+    prev = ctypes.c_int(7)
+    assert L.net2_sha2_set_device(-1, ctypes.byref(prev)) == 0 and prev.value == -1
+    assert L.net2_sha2_set_device(0, None) == errno.ENODEV
+    assert L.net2_sha2_get_device(None) == errno.EINVAL
+    assert L.net2_sha2_get_device(ctypes.byref(prev)) == errno.ENODEV
+
+
+def test_partial_abi_build_is_refused(tmp_path):
+    """A build lacking entry points of this ABI (NET2_SHA2_LIB pointed at an
+    older round's library) is refused, naming what it lacks, unless the A/B
+    opt-in is set."""
+    so = tmp_path / "libpartial.so"
+    src = tmp_path / "partial.c"
+    src.write_text("int net2_sha2_abi_version(void) { return 1; }\n")
+    import subprocess
+    subprocess.run(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)], check=True)
+    with pytest.raises(ImportError) as ei:
+        _lib.bind(ctypes.CDLL(str(so)))
+    assert "net2_sha2_batch" in str(ei.value)
+    h2 = _lib.bind(ctypes.CDLL(str(so)), allow_old_abi=True)
+    assert h2.net2_sha2_abi_version() == 1
 
 
 @pytest.mark.skipif(_lib.device_count() > 0, reason="a GPU is present")

@@ -26,6 +26,17 @@ def show(name, p):
           f"devptr={a.devicePointer or 0:#x} hostptr={a.hostPointer or 0:#x} "
           f"flags={a.allocationFlags:#x} | getdevptr rc={rc2} dp={dp.value or 0:#x} "
           f"delta={(dp.value or 0) - p}", flush=True)
+    # allocation range / buffer id (sha2_shim.cpp pinned_span)
+    for nm, code in (("RANGE_START_ADDR", 11), ("RANGE_SIZE", 12), ("BUFFER_ID", 7)):
+        v = ctypes.c_uint64(0)
+        rc3 = hip.hipPointerGetAttribute(ctypes.byref(v), ctypes.c_int(code),
+                                         ctypes.c_void_p(p))
+        print(f"    {nm:16s} rc={rc3} v={v.value:#x}", flush=True)
+    base = ctypes.c_void_p()
+    size = ctypes.c_size_t()
+    rc4 = hip.hipMemGetAddressRange(ctypes.byref(base), ctypes.byref(size), ctypes.c_void_p(p))
+    print(f"    hipMemGetAddressRange rc={rc4} base={base.value or 0:#x} size={size.value:#x}",
+          flush=True)
 
 
 t = torch.empty(1 << 20, dtype=torch.uint8).pin_memory()
@@ -38,5 +49,14 @@ print("register rc", int(cr.cudaHostRegister(a0, 1 << 20, 0)), flush=True)
 show("registered start", a0)
 show("registered +13", a0 + 13)
 show("registered +65536+13", a0 + 65536 + 13)
+show("registered last byte", a0 + (1 << 20) - 1)
+show("registered one past", a0 + (1 << 20))
 print("unregister rc", int(cr.cudaHostUnregister(a0)), flush=True)
 show("pageable", buf.ctypes.data)
+# two pinned allocations back to back: is the second one's start the first's end?
+u = torch.empty(4096, dtype=torch.uint8).pin_memory()
+v = torch.empty(4096, dtype=torch.uint8).pin_memory()
+print(f"adjacent pinned: u={u.data_ptr():#x} v={v.data_ptr():#x} "
+      f"gap={v.data_ptr() - u.data_ptr()}", flush=True)
+show("u last byte", u.data_ptr() + 4095)
+show("v first byte", v.data_ptr())
