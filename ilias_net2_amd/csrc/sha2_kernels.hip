@@ -1723,6 +1723,241 @@ __global__ __launch_bounds__(256) void burst_final_kernel(uint64_t n,
 	result[i] = (uint8_t)st;
 }
 
+/* ---- small bursts: one workgroup per datagram ---------------------------- */
+
+/*
+ * Latency form of the keyed burst modes (HMAC_BURST_RX / HMAC_BURST_TX of
+ * hmac_kernel, plus burst_final_kernel's fold and IV): for a burst of at
+ * most one datagram per SIMD, whose time is one datagram's serial chain of
+ * compressions on one lane (~100 us for a 1,500-byte HMAC-SHA512 datagram,
+ * profiles/round6/burst_sizes_*.jsonl), whatever the lane layout.  Here the
+ * datagram gets a workgroup of two waves:
+ *   wave 0 -- the HMAC: its lanes expand up to BW_NB blocks of the message at
+ *     once (lane b: block c0 + b, loaded, padded and expanded into its K + W
+ *     row in LDS; a block's schedule depends only on its own words), then the
+ *     wave runs only the rounds, block after block, from LDS (as
+ *     job_wave_kernel does for the coalescer); then the outer block, the
+ *     verdict (RX) or the hash field (TX), and every store of the datagram;
+ *   wave 1 -- RX: the datagram's IV from its header (two SHA-256
+ *     compressions, ph_iv_one) into LDS meanwhile, off wave 0's chain.
+ * Codes, decoded headers, IVs and sealed fields are those of hmac_item +
+ * burst_final_kernel (RX) / hmac_item (TX), bit for bit.
+ *
+ * rx: RX -- seq / flags receive the decoded header (NULL: not stored);
+ * TX -- seq / flags are the inputs, rec as in BurstArgs (the host path) or
+ * NULL (header and hash field written into out == base).  result: the final
+ * code per datagram (RX always; TX without rec).
+ */
+#define BW_NB 16	/* blocks expanded per pass (LDS rows) */
+
+/* Block k of an inner message of mlen bytes at m (nfull whole blocks, rem
+ * tail bytes, bit count `bits` incl. the key block) as big-endian words. */
+template <class H>
+__device__ __forceinline__ void bw_block(const uint8_t *m, uint32_t k,
+    uint32_t nfull, uint32_t rem, uint32_t nb, uint64_t bits,
+    uint32_t (&w)[H::NW32])
+{
+	constexpr int NW32 = H::NW32;
+	if (k < nfull) {
+		const uint8_t *bp = m + (size_t)k * H::BLOCK;
+		Raw<NW32> r;
+		issue_block<NW32, AMODE_A1>(bp, r);
+		finish_block<NW32, AMODE_A1>(bp, r, w);
+		return;
+	}
+	if (k == nfull) {
+		tail_block<NW32>(m + (size_t)nfull * H::BLOCK, rem, w);
+	} else {
+#pragma unroll
+		for (int i = 0; i < NW32; i++)
+			w[i] = 0;
+	}
+	if (k == nb - 1) {
+		w[NW32 - 2] = (uint32_t)(bits >> 32);
+		w[NW32 - 1] = (uint32_t)bits;
+	}
+}
+
+/* LDS written by some lanes of a wave, read by others of the same wave. */
+__device__ __forceinline__ void wave_lds_sync()
+{
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+template <class H, int MODE, bool IS384>
+__global__ __launch_bounds__(128) void burst_wave_kernel(
+    const uint8_t *__restrict__ base, const uint64_t *__restrict__ offsets,
+    const uint32_t *__restrict__ lens, HMid hm, BurstArgs rx,
+    uint8_t *__restrict__ result, uint8_t *__restrict__ iv, uint32_t ivlen,
+    uint8_t *__restrict__ out)
+{
+	constexpr int NW32 = H::NW32;
+	typedef typename H::word W;
+	constexpr int ROW = sizeof(W) == 4 ? NET2_JOB_ROW256 : NET2_JOB_ROW512;
+	constexpr uint32_t dlen = sizeof(W) == 4 ? 32 : IS384 ? 48 : 64;
+	__shared__ W rows[BW_NB * ROW];
+	__shared__ uint32_t mid[4][16];
+	__shared__ uint32_t ivw[16];
+	if (threadIdx.x == 0) {
+		constexpr int NK = MODE == HMAC_BURST_RX ? 4 : 2;
+		constexpr int NWD = sizeof(W) == 4 ? 8 : 16;
+#pragma unroll
+		for (int k = 0; k < NK; k++)
+#pragma unroll
+			for (int j = 0; j < NWD; j++)
+				mid[k][j] = hm.w[k][j];
+	}
+	if (sizeof(W) == 8)
+		k512_lds_fill();	/* (synchronises the workgroup) */
+	else
+		__syncthreads();
+	const uint32_t lane = threadIdx.x & 63;
+	const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const uint64_t i = blockIdx.x;
+	const uint64_t off = offsets[i];
+	uint32_t len = lens[i];
+	const uint8_t *p = base + off;
+	uint32_t st = PKT_OK, seq = 0, fl = 0;
+	const uint32_t (*lmid)[16] = mid;
+	if (MODE == HMAC_BURST_TX) {
+		seq = rx.seq[i];
+		fl = rx.flags[i];
+		const bool sg = (fl & PKT_PH_SIGNED) != 0;
+		const bool cr = (fl & PKT_PH_ENCRYPTED) != 0;
+		if (!sg || cr != (rx.enc_set != 0))
+			st = PKT_UNSAFE;
+		else if (len < 8 + dlen)
+			st = PKT_RESOURCE;	/* no room for header and hash */
+	} else {
+		if (len < 8) {
+			st = PKT_BAD;		/* header decode fails */
+		} else {
+			seq = load_be32_bytes(p);
+			fl = load_be32_bytes(p + 4);
+		}
+		/* net2_ck_rx_key (src/conn_keys.c:447-476) */
+		const bool use_alt = st == PKT_OK && rx.alt &&
+		    ((fl & PKT_PH_ALTKEY) != 0 || (!rx.no_cutoff &&
+		    seq - rx.rx_start >= rx.cutoff - rx.rx_start));
+		if (use_alt)
+			lmid = mid + 2;
+		const int enc_set = use_alt ? rx.alt_enc_set : rx.enc_set;
+		if (st == PKT_OK && ((fl & PKT_PH_SIGNED) == 0 ||
+		    (enc_set && (fl & PKT_PH_ENCRYPTED) == 0)))
+			st = PKT_UNSAFE;
+	}
+	const bool ok = st == PKT_OK;
+	/* the datagram's region after the header: hash field, then message */
+	const uint32_t rlen = ok ? len - 8 : 0;
+	const bool short_dgram = rlen < dlen;
+	const uint8_t *field = p + 8;
+	const uint8_t *m = field + dlen;
+	const uint32_t mlen = short_dgram ? 0 : rlen - dlen;
+
+	if (wv == 1) {
+		/* RX: the IV of an encrypted datagram that may verify */
+		if (MODE == HMAC_BURST_RX && ok && ivlen > 0 && iv != nullptr &&
+		    (fl & PKT_PH_ENCRYPTED) && lane == 0)
+			ph_iv_one(seq, fl, ivlen, reinterpret_cast<uint8_t *>(ivw));
+		__syncthreads();
+		return;
+	}
+
+	/* wave 0: HMAC of the message from the ipad midstate (a datagram
+	 * already refused, or without room for its hash field, hashes nothing) */
+	const bool hashed = ok && !short_dgram;
+	typename H::State s;
+	load_mid<H>(lmid, 0, s);
+	const uint32_t nfull = mlen / H::BLOCK;
+	const uint32_t rem = mlen % H::BLOCK;
+	const uint32_t nb = !hashed ? 0 : nfull + 1 +
+	    (rem >= (uint32_t)(H::BLOCK - H::LENBYTES) ? 1 : 0);
+	const uint64_t bits = ((uint64_t)mlen + H::BLOCK) << 3;
+	for (uint32_t c0 = 0; c0 < nb; c0 += BW_NB) {
+		const uint32_t k = c0 + lane;
+		if (lane < BW_NB && k < nb) {
+			uint32_t w[NW32];
+			bw_block<H>(m, k, nfull, rem, nb, bits, w);
+			sched_row<H>(w, rows + lane * ROW);
+		}
+		wave_lds_sync();
+		const uint32_t cnt = min((uint32_t)BW_NB, nb - c0);
+		for (uint32_t b = 0; b < cnt; b++)
+			rounds_row<H>(s, rows + b * ROW);
+		wave_lds_sync();
+	}
+	/* outer: one block = inner digest || 0x80 || 0... || bit count */
+	if (hashed) {
+		uint32_t w[NW32];
+#pragma unroll
+		for (int j = 0; j < NW32; j++)
+			w[j] = 0;
+		const int dw = digest_words<H>(s, IS384, w);
+#pragma unroll
+		for (int j = 12; j < 16; j++)		/* SHA-384 keeps 12 words */
+			if (j >= dw)
+				w[j] = 0;
+		w[dw] = 0x80000000u;
+		const uint64_t obits = (uint64_t)(H::BLOCK + 4 * dw) << 3;
+		w[NW32 - 2] = (uint32_t)(obits >> 32);
+		w[NW32 - 1] = (uint32_t)obits;
+		load_mid<H>(lmid, 1, s);
+		H::compress(s, w);
+	}
+	uint32_t o[16];
+	H::out_words(s, o, IS384);
+	__syncthreads();		/* wave 1's IV is in LDS */
+	if (lane != 0)
+		return;
+	if (MODE == HMAC_BURST_RX) {
+		uint32_t code = st;
+		if (ok) {		/* net2_buffer_cmp, packet.n2t:253-257 */
+			uint32_t diff = 0;
+			if (hashed) {
+#pragma unroll
+				for (uint32_t j = 0; j < dlen; j++)
+					diff |= field[j] ^
+					    ((o[j >> 2] >> (8 * (j & 3))) & 0xffu);
+			}
+			code = !hashed || diff != 0 ? PKT_BAD : PKT_OK;
+		}
+		if (rx.seq != nullptr) {
+			rx.seq[i] = seq;
+			rx.flags[i] = fl;
+		}
+		if (code == PKT_OK && ivlen > 0 && iv != nullptr &&
+		    (fl & PKT_PH_ENCRYPTED)) {
+			const uint8_t *src = reinterpret_cast<const uint8_t *>(ivw);
+			uint8_t *dst = iv + i * ivlen;
+			for (uint32_t b = 0; b < ivlen; b++)
+				dst[b] = src[b];
+		}
+		result[i] = (uint8_t)code;
+		return;
+	}
+	/* TX */
+	if (rx.rec != nullptr) {
+		uint8_t *r = rx.rec + i * (dlen + 16);
+		if (hashed)
+			store_digest<dlen>(r, o);
+		*reinterpret_cast<uint4 *>(r + dlen) = make_uint4(
+		    ok ? bswap32(seq) : 0u, ok ? bswap32(fl) : 0u, (uint32_t)i, st);
+		return;
+	}
+	if (hashed) {
+		uint8_t *h = out + off;
+#pragma unroll
+		for (int b = 0; b < 4; b++) {
+			h[b] = (uint8_t)(seq >> (24 - 8 * b));
+			h[4 + b] = (uint8_t)(fl >> (24 - 8 * b));
+		}
+		store_digest<dlen>(h + 8, o);
+	}
+	result[i] = (uint8_t)st;
+}
+
 /* ---- length binning (counting sort by block count, longest first) ---- */
 
 __device__ __forceinline__ uint32_t bin_of(uint32_t len, int blk_shift,
@@ -2586,6 +2821,87 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 	}
 	return hipGetLastError();
 }
+template <class H, bool IS384>
+static void launch_burst_wave(int mode, uint64_t n, hipStream_t s,
+    const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
+    const HMid &hm, const BurstArgs &a, uint8_t *result, uint8_t *iv,
+    uint32_t ivlen, uint8_t *out)
+{
+	if (mode == HMAC_BURST_RX)
+		burst_wave_kernel<H, HMAC_BURST_RX, IS384><<<(unsigned)n, 128, 0, s>>>(
+		    base, offsets, lens, hm, a, result, iv, ivlen, out);
+	else
+		burst_wave_kernel<H, HMAC_BURST_TX, IS384><<<(unsigned)n, 128, 0, s>>>(
+		    base, offsets, lens, hm, a, result, iv, ivlen, out);
+}
+
+uint64_t net2_burst_wave_max(void)
+{
+	/* read per call (a test compares both forms in one process) */
+	const char *e = getenv("NET2_BURST_WAVE_MAX");
+	if (e != nullptr && *e != '\0')
+		return strtoull(e, nullptr, 10);
+	/* one datagram per SIMD: beyond that the wave form's datagrams share
+	 * SIMDs while the lane form's latency does not grow until ~64x more */
+	static std::atomic<int> cus[64];
+	int dev = 0;
+	if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+		(void)hipGetLastError();
+		return 0;
+	}
+	int c = cus[dev].load(std::memory_order_relaxed);
+	if (c == 0) {
+		if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount,
+		    dev) != hipSuccess || c <= 0) {
+			(void)hipGetLastError();
+			return 0;
+		}
+		cus[dev].store(c, std::memory_order_relaxed);
+	}
+	return (uint64_t)c * 4;
+}
+
+hipError_t net2_launch_burst_wave(int alg, const uint8_t *key, size_t keylen,
+    const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
+    uint64_t n, const BurstArgs *args, uint8_t *result, uint8_t *iv,
+    uint32_t ivlen, uint8_t *out, int mode, hipStream_t s)
+{
+	if ((mode != HMAC_BURST_RX && mode != HMAC_BURST_TX) || args == nullptr ||
+	    offsets == nullptr || ivlen > 64 || n > 0x7fffffffu)
+		return hipErrorInvalidValue;
+	if (mode == HMAC_BURST_RX && args->rec != nullptr)
+		return hipErrorInvalidValue;
+	if (n == 0)
+		return hipSuccess;
+	const int halg = alg - 3;	/* HMAC row -> SHA row */
+	const int blk = halg == NET2_ALG_SHA256 ? 64 : 128;
+	if (halg < NET2_ALG_SHA256 || halg > NET2_ALG_SHA512 ||
+	    keylen > (size_t)blk)
+		return hipErrorInvalidValue;
+	uint8_t kb[128] = { 0 };
+	for (size_t j = 0; j < keylen; j++)
+		kb[j] = key[j];
+	HMid hm = {};
+	hmac_midstates(halg, kb, &hm, 0);
+	if (mode == HMAC_BURST_RX && args->alt) {
+		uint8_t ab[128] = { 0 };
+		for (int j = 0; j < 32; j++)	/* K' as big-endian words */
+			for (int b = 0; b < 4; b++)
+				ab[4 * j + b] = (uint8_t)(args->altkey[j] >> (24 - 8 * b));
+		hmac_midstates(halg, ab, &hm, 2);
+	}
+	if (halg == NET2_ALG_SHA256)
+		launch_burst_wave<Sha256H, false>(mode, n, s, base, offsets, lens,
+		    hm, *args, result, iv, ivlen, out);
+	else if (halg == NET2_ALG_SHA384)
+		launch_burst_wave<Sha512H, true>(mode, n, s, base, offsets, lens,
+		    hm, *args, result, iv, ivlen, out);
+	else
+		launch_burst_wave<Sha512H, false>(mode, n, s, base, offsets, lens,
+		    hm, *args, result, iv, ivlen, out);
+	return hipGetLastError();
+}
+
 hipError_t net2_launch_jobs(const uint8_t *stage, const Net2Job *jobs,
     uint32_t n256, uint32_t n512, uint8_t *out, uint32_t *done, int wave,
     hipStream_t s, uint32_t chunk)

@@ -130,6 +130,26 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
     const BurstArgs *burst_args = nullptr);
 
 /*
+ * Small keyed bursts (net2_packet_{decode,encode}_burst with a hash key, at
+ * most net2_burst_wave_max() datagrams): one workgroup per datagram
+ * (burst_wave_kernel) instead of one lane -- the burst's time is one
+ * datagram's chain either way, and the wave form shortens it by expanding
+ * the message schedules in parallel.  mode NET2_HMAC_MODE_BURST_RX / _TX;
+ * args as for net2_launch_hmac (RX: seq / flags receive the decoded headers,
+ * either may be NULL together; TX: the inputs, and rec).  result: the final
+ * code per datagram (RX; TX without rec); iv: RX IVs (ivlen <= 64; NULL or
+ * 0: none); out: TX without rec, the datagrams sealed in place (== base).
+ * No workspace, no separate fold / IV launch.
+ */
+hipError_t net2_launch_burst_wave(int alg, const uint8_t *key, size_t keylen,
+    const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
+    uint64_t n, const BurstArgs *args, uint8_t *result, uint8_t *iv,
+    uint32_t ivlen, uint8_t *out, int mode, hipStream_t s);
+/* The largest burst net2_launch_burst_wave is for on the current device:
+ * one datagram per SIMD (NET2_BURST_WAVE_MAX overrides; 0: never). */
+uint64_t net2_burst_wave_max(void);
+
+/*
  * Coalesced small jobs (sha2_coalesce.cpp): many independent requests from
  * host threads, each already laid out by the host as whole blocks in one
  * staging buffer.  Job j: nblk blocks at stage + data, compressed from the

@@ -1772,6 +1772,21 @@ int decode_burst(const struct net2_burst_rx_keys *k, uint32_t ivlen,
 			for (size_t i = 0; i < k->alt_hash_keylen; i++)
 				rx.altkey[i / 4] |= (uint32_t)ak[i] << (24 - 8 * (i % 4));
 		}
+		if (n <= net2_burst_wave_max()) {
+			/* a small burst: one workgroup per datagram, codes, headers
+			 * and IVs stored by that one launch */
+			rx.seq = d_seq;
+			rx.flags = d_flags;
+			rx.status = nullptr;
+			HIP_TRY(net2_launch_burst_wave(hash_alg,
+			    (const uint8_t *)k->hash_key, k->hash_keylen,
+			    (const uint8_t *)d_base, d_offsets, d_lens, n, &rx,
+			    d_result, enc_set ? (uint8_t *)d_iv : nullptr,
+			    enc_set ? ivlen : 0, nullptr, NET2_HMAC_MODE_BURST_RX,
+			    s));
+			FI_POINT(FI_KERNEL);
+			return 0;
+		}
 		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)k->hash_key,
 		    k->hash_keylen, (const uint8_t *)d_base, d_offsets, d_lens, 0,
 		    0, n, w.verdict, burst_bins(n, w.bin), s,
@@ -1810,6 +1825,16 @@ int encode_burst(int hash_alg, const void *hash_key, size_t hash_keylen,
 		tx.status = d_result;
 		tx.enc_set = enc_alg != 0;
 		tx.rec = rec;
+		if (n <= net2_burst_wave_max()) {
+			/* a small burst: one workgroup per datagram */
+			HIP_TRY(net2_launch_burst_wave(hash_alg,
+			    (const uint8_t *)hash_key, hash_keylen,
+			    (const uint8_t *)d_base, d_offsets, d_lens, n, &tx,
+			    d_result, nullptr, 0, (uint8_t *)d_base,
+			    NET2_HMAC_MODE_BURST_TX, s));
+			FI_POINT(FI_KERNEL);
+			return 0;
+		}
 		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)hash_key,
 		    hash_keylen, (const uint8_t *)d_base, d_offsets, d_lens, 0,
 		    0, n, (uint8_t *)d_base, burst_bins(n, w.bin), s,
@@ -2251,6 +2276,7 @@ int run_burst_slice(size_t didx, int ordinal, const HostBurst &hb,
 	/* outputs are stored through their mapping only when the slice's
 	 * whole range of each is in one page-locked allocation */
 	const uint64_t m = hi - lo;
+	const double tq0 = dbg_now();
 	BurstPins pins;
 	pins.base = is_pinned(hb.base);
 	pins.result = pinned_span(hb.result + lo, m);
@@ -2263,6 +2289,9 @@ int run_burst_slice(size_t didx, int ordinal, const HostBurst &hb,
 		pins.flags = hb.flags_out != nullptr && pinned_span(hb.flags_out +
 		    lo, m * 4);
 	}
+	if (dbg_timing())
+		fprintf(stderr, "net2 burst: page-lock lookups %.3f ms\n",
+		    dbg_now() - tq0);
 	const PackPlan all = pack_sizes(*c->pool, hb.lens + lo, hi - lo);
 	const size_t mean = std::max<size_t>(all.start[all.nt] /
 	    std::max<uint64_t>(hi - lo, 1), 16);
