@@ -1720,18 +1720,16 @@ int check_burst_args(int hash_alg, const void *key, size_t keylen,
 
 /*
  * The binning workspace a burst's HMAC kernel is given: below
- * NET2_BURST_BIN_MIN datagrams (default 4,096, as net2_sha2_batch's
- * host path) none -- the batch is a few waves on an otherwise idle chip,
- * its time is its longest wave's whatever the order, and the binning
- * launch is pure fixed cost (tools/burst_sizes.py).
+ * NET2_BURST_BIN_MIN datagrams (default 65,536: one lane per datagram, one
+ * wave per SIMD) none -- every wave then has a SIMD of its own, the burst
+ * takes its longest wave's time whatever the order, and the binning launch
+ * is pure fixed cost (tools/burst_sizes.py).  Read per call.
  */
 uint32_t *burst_bins(uint64_t n, uint32_t *bin)
 {
-	static const uint64_t min_n = []() {
-		const char *e = getenv("NET2_BURST_BIN_MIN");
-		return e != nullptr && *e != '\0' ? strtoull(e, nullptr, 10) :
-		    (uint64_t)4096;
-	}();
+	const char *e = getenv("NET2_BURST_BIN_MIN");
+	const uint64_t min_n = e != nullptr && *e != '\0' ?
+	    strtoull(e, nullptr, 10) : (uint64_t)65536;
 	return n >= min_n ? bin : nullptr;
 }
 
@@ -1773,8 +1771,8 @@ int decode_burst(const struct net2_burst_rx_keys *k, uint32_t ivlen,
 				rx.altkey[i / 4] |= (uint32_t)ak[i] << (24 - 8 * (i % 4));
 		}
 		if (n <= net2_burst_wave_max()) {
-			/* a small burst: one workgroup per datagram, codes, headers
-			 * and IVs stored by that one launch */
+			/* a small burst: one workgroup per datagram, codes,
+			 * headers and IVs stored by that one launch */
 			rx.seq = d_seq;
 			rx.flags = d_flags;
 			rx.status = nullptr;

@@ -103,13 +103,14 @@ def _burst(n, seed, hash_alg, enc_set):
     return data, offs.astype(np.uint64), slot, seq, flags, rng
 
 
-@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 333, 1024])
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 333, 1024, 2047, 5000, 16384, 16385])
 @pytest.mark.parametrize("hash_alg,enc_set,ivlen", [(6, True, 16), (4, True, 32),
                                                     (5, False, 0)])
 def test_small_host_bursts_default_threshold(dev, oracle_mod, n, hash_alg, enc_set,
                                              ivlen):
     """Integration-sized bursts at the default threshold (the wave form up
-    to one datagram per SIMD): TX, then RX with tampered bytes and runts,
+    to one datagram per SIMD, the lane form above, unbinned below 65,536
+    datagrams): TX, then RX with tampered bytes and runts,
     pinned and pageable buffers, every code / sealed byte / header / IV
     against the oracle.  Message lengths straddle the padding boundaries
     (55/56, 111/112, 119/120 bytes: the length field in the tail block or a

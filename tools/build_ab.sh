@@ -9,7 +9,7 @@ HERE=$(cd "$(dirname "$0")" && pwd)
 SRC=$HERE/../ilias_net2_amd/csrc
 mkdir -p $HERE/ab
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden \
-    -Wall -Wno-unused-result -cuid=net2sha2 "$@" -c $SRC/sha2_kernels.hip -o $HERE/ab/$name.o
+    -Wall -Wno-unused-result -cuid=net2sha2 "$@" -c ${KSRC:-$SRC/sha2_kernels.hip} -o $HERE/ab/$name.o
 # build id: hash of the device code, as the Makefile stamps it
 /opt/rocm/lib/llvm/bin/llvm-objcopy --dump-section=.hip_fatbin=$HERE/ab/$name.fatbin \
     $HERE/ab/$name.o $HERE/ab/$name.tmp.o && rm -f $HERE/ab/$name.tmp.o
