@@ -87,3 +87,52 @@ def test_no_counters_file(joined):
     assert roof["traffic"] is None and valu is None
     # the algorithmic side is there regardless
     assert roof["frac"] == pytest.approx(815e6 / 0.7155e-3 / 1e9 / 8000, abs=1e-4)
+
+
+def test_trace_box_at_another_clock_is_refused(joined):
+    """The kernel trace committed beside the counters must come from a box
+    that timed the config within 3 % of this line's clock (VERDICT round 5,
+    item 5): the PMC clock alone agreeing is not enough."""
+    pmc = _pmc()
+    pmc["trace_box"]["sclk_mhz_during_timed_steps"] = 2250
+    pmc["trace_avg_ns"] = 790_100.0
+    roof, valu = joined(pmc)
+    assert roof["traffic"] is None and valu is None
+    assert "trace box" in roof["traffic_note"]
+    pmc["trace_box"]["sclk_mhz_during_timed_steps"] = 2330
+    roof, _ = joined(pmc)
+    assert roof["traffic"] == 1.5e9
+    assert roof["trace_kernel_ms"] == pytest.approx(0.7901)
+
+
+def test_line_tail_keeps_every_config():
+    """finalize_line: prose moves to one notes object, the contract's fields
+    stay, and the closing summary carries every config's numbers, so the
+    last ~2 KB of the printed line hold C3 / C4."""
+    import json
+    line = {"metric": "m", "value": 1.0, "unit": "digests/s", "n_gpus": 1,
+            "ms_per_step": 0.6, "config": {"workload": "w" * 100},
+            "roofline": {"frac": 0.22, "kernel_ms": 0.61},
+            "cpu_baseline": {"value": 7.7e6, "unit": "digests/s", "cores": 16,
+                             "kind": "port", "sample": "s" * 300,
+                             "openssl_context": {"note": "n" * 200, "value": 1.0}},
+            "extra_configs": {
+                "c3": {"value": 2.28e9, "ms_per_step": 0.46, "metric": "x" * 120,
+                       "roofline": {"frac": 0.209, "kernel_ms": 0.455,
+                                    "traffic_over_algorithmic": 1.54},
+                       "cpu_baseline": {"value": 1.1e7, "sample": "y" * 200}},
+                "c4": {"value": 1.36e9, "ms_per_step": 0.77,
+                       "roofline": {"frac": 0.185, "kernel_ms": 0.771}},
+                "burst_rx_e2e": {"value": 7.2e7, "ms_per_step": 14.4,
+                                 "pageable": {"value": 6.9e7}}}}
+    out = bench.finalize_line(line)
+    text = json.dumps(out)
+    tail = text[-2000:]
+    for want in ('"c3": {"value": 2280000000.0', '"frac": 0.209', '"c4"',
+                 '"burst_rx_e2e"'):
+        assert want in tail, want
+    assert list(out)[-1] == "summary"
+    assert out["cpu_baseline"]["sample"] == "s" * 300          # contract field kept
+    assert "extra_configs.c3.metric" in out["notes"]
+    assert "cpu_baseline.openssl_context.note" in out["notes"]
+    assert list(out).index("notes") < list(out).index("roofline")
