@@ -1723,35 +1723,52 @@ __global__ __launch_bounds__(256) void burst_final_kernel(uint64_t n,
 	result[i] = (uint8_t)st;
 }
 
-/* ---- small bursts: one workgroup per datagram ---------------------------- */
+/* ---- small bursts: a few datagrams per workgroup ------------------------- */
 
 /*
  * Latency form of the keyed burst modes (HMAC_BURST_RX / HMAC_BURST_TX of
- * hmac_kernel, plus burst_final_kernel's fold and IV): for a burst of at
- * most one datagram per SIMD, whose time is one datagram's serial chain of
- * compressions on one lane (~100 us for a 1,500-byte HMAC-SHA512 datagram,
- * profiles/round6/burst_sizes_*.jsonl), whatever the lane layout.  Here the
- * datagram gets a workgroup of two waves:
- *   wave 0 -- the HMAC: its lanes expand up to BW_NB blocks of the message at
- *     once (lane b: block c0 + b, loaded, padded and expanded into its K + W
- *     row in LDS; a block's schedule depends only on its own words), then the
- *     wave runs only the rounds, block after block, from LDS (as
- *     job_wave_kernel does for the coalescer); then the outer block, the
- *     verdict (RX) or the hash field (TX), and every store of the datagram;
- *   wave 1 -- RX: the datagram's IV from its header (two SHA-256
- *     compressions, ph_iv_one) into LDS meanwhile, off wave 0's chain.
+ * hmac_kernel, plus burst_final_kernel's fold and IV), for bursts of at most
+ * BW_GMAX datagrams per SIMD.  A burst that small has at most one wave per
+ * SIMD in the lane form too, so its time is one datagram's serial chain of
+ * compressions, schedule expansion included (~100 us for a 1,500-byte
+ * HMAC-SHA512 datagram, profiles/round6/burst_sizes_*.jsonl).  Here a
+ * workgroup of two waves takes G datagrams (G <= BW_GMAX, chosen by the
+ *   launcher so that the grid is about one workgroup per SIMD):
+ *   wave 0 -- lane l runs datagram (l mod G)'s HMAC, so every datagram's
+ *     rounds run on 64 / G lanes in lockstep and no lane idles: rounds on
+ *     one lane of a wave (an EXEC mask of one) ran 27 % slower per wave and,
+ *     with four workgroups per CU, twice as slow (profiles/round6/bwp_*:
+ *     89 / 176 us at 64 / 1,024 datagrams against 70 / 74).  Each pass, the
+ *     wave's lanes first expand K = BW_ROWS / G blocks of every one of the G
+ *     messages at once (row r: datagram r / K, block c0 + r % K, loaded,
+ *     padded and expanded into its K + W row in LDS -- a block's schedule
+ *     depends only on its own words), then every lane runs the rounds of
+ *     its datagram's K blocks from LDS; lane d < G stores datagram d.  A pass costs one row's expansion however many rows
+ *     it fills, so the schedule work leaves the serial chain: a 12-block
+ *     datagram takes one pass at G <= 4, five at G = 16, against twelve
+ *     expansions in the lane form.  Then the outer block, the verdict (RX)
+ *     or the hash field (TX), and every store of the datagram;
+ *   wave 1 -- RX: lane d derives datagram d's IV from its header (two
+ *     SHA-256 compressions, ph_iv_one) into LDS meanwhile, off the chain.
  * Codes, decoded headers, IVs and sealed fields are those of hmac_item +
- * burst_final_kernel (RX) / hmac_item (TX), bit for bit.
+ * burst_final_kernel (RX) / hmac_item (TX), bit for bit; the datagrams of a
+ * workgroup are consecutive (no binning: the burst's time is its longest
+ * datagram's either way).
  *
  * rx: RX -- seq / flags receive the decoded header (NULL: not stored);
  * TX -- seq / flags are the inputs, rec as in BurstArgs (the host path) or
  * NULL (header and hash field written into out == base).  result: the final
- * code per datagram (RX always; TX without rec).
+ * code per datagram (RX; TX without rec).
  */
-#define BW_NB 16	/* blocks expanded per pass (LDS rows) */
+#define BW_ROWS 48	/* K + W rows of LDS per workgroup (31 KB at SHA-512:
+			 * four workgroups per CU; 16 rows measured no faster,
+			 * profiles/round6/bw_w2r16_*.jsonl) */
+#define BW_GMAX 16	/* datagrams per workgroup at most: at G = 32 a pass
+			 * expands one block per datagram, the lane form's cost */
 
 /* Block k of an inner message of mlen bytes at m (nfull whole blocks, rem
- * tail bytes, bit count `bits` incl. the key block) as big-endian words. */
+ * tail bytes, nb blocks, bit count `bits` incl. the key block) as
+ * big-endian words. */
 template <class H>
 __device__ __forceinline__ void bw_block(const uint8_t *m, uint32_t k,
     uint32_t nfull, uint32_t rem, uint32_t nb, uint64_t bits,
@@ -1786,20 +1803,75 @@ __device__ __forceinline__ void wave_lds_sync()
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+/* One datagram's header, key choice and the region its HMAC covers. */
+struct BwDgram {
+	uint32_t st, seq, fl;
+	bool ok, hashed, alt;
+	uint64_t off;		/* datagram start */
+	uint32_t mlen;		/* message bytes after header and hash field */
+};
+
+template <int MODE, uint32_t DLEN>
+__device__ __forceinline__ BwDgram bw_decode(const uint8_t *__restrict__ base,
+    const uint64_t *__restrict__ offsets, const uint32_t *__restrict__ lens,
+    uint64_t i, const BurstArgs &rx)
+{
+	BwDgram g;
+	g.off = offsets[i];
+	const uint32_t len = lens[i];
+	const uint8_t *p = base + g.off;
+	g.st = PKT_OK;
+	g.seq = g.fl = 0;
+	g.alt = false;
+	if (MODE == HMAC_BURST_TX) {
+		g.seq = rx.seq[i];
+		g.fl = rx.flags[i];
+		const bool sg = (g.fl & PKT_PH_SIGNED) != 0;
+		const bool cr = (g.fl & PKT_PH_ENCRYPTED) != 0;
+		if (!sg || cr != (rx.enc_set != 0))
+			g.st = PKT_UNSAFE;
+		else if (len < 8 + DLEN)
+			g.st = PKT_RESOURCE;	/* no room for header and hash */
+	} else {
+		if (len < 8) {
+			g.st = PKT_BAD;		/* header decode fails */
+		} else {
+			g.seq = load_be32_bytes(p);
+			g.fl = load_be32_bytes(p + 4);
+		}
+		/* net2_ck_rx_key (src/conn_keys.c:447-476) */
+		g.alt = g.st == PKT_OK && rx.alt &&
+		    ((g.fl & PKT_PH_ALTKEY) != 0 || (!rx.no_cutoff &&
+		    g.seq - rx.rx_start >= rx.cutoff - rx.rx_start));
+		const int enc_set = g.alt ? rx.alt_enc_set : rx.enc_set;
+		if (g.st == PKT_OK && ((g.fl & PKT_PH_SIGNED) == 0 ||
+		    (enc_set && (g.fl & PKT_PH_ENCRYPTED) == 0)))
+			g.st = PKT_UNSAFE;
+	}
+	g.ok = g.st == PKT_OK;
+	/* after the header: hash field, then message */
+	const uint32_t rlen = g.ok ? len - 8 : 0;
+	g.hashed = g.ok && rlen >= DLEN;
+	g.mlen = g.hashed ? rlen - DLEN : 0;
+	return g;
+}
+
 template <class H, int MODE, bool IS384>
 __global__ __launch_bounds__(128) void burst_wave_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offsets,
-    const uint32_t *__restrict__ lens, HMid hm, BurstArgs rx,
-    uint8_t *__restrict__ result, uint8_t *__restrict__ iv, uint32_t ivlen,
-    uint8_t *__restrict__ out)
+    const uint32_t *__restrict__ lens, uint64_t n, uint32_t G, HMid hm,
+    BurstArgs rx, uint8_t *__restrict__ result, uint8_t *__restrict__ iv,
+    uint32_t ivlen, uint8_t *__restrict__ out)
 {
 	constexpr int NW32 = H::NW32;
 	typedef typename H::word W;
 	constexpr int ROW = sizeof(W) == 4 ? NET2_JOB_ROW256 : NET2_JOB_ROW512;
 	constexpr uint32_t dlen = sizeof(W) == 4 ? 32 : IS384 ? 48 : 64;
-	__shared__ W rows[BW_NB * ROW];
+	__shared__ W rows[BW_ROWS * ROW];
 	__shared__ uint32_t mid[4][16];
-	__shared__ uint32_t ivw[16];
+	__shared__ uint32_t ivw[BW_GMAX][16];
+	__shared__ uint64_t geo_m[BW_GMAX];	/* message start (offset) */
+	__shared__ uint32_t geo_len[BW_GMAX], geo_nb[BW_GMAX];
 	if (threadIdx.x == 0) {
 		constexpr int NK = MODE == HMAC_BURST_RX ? 4 : 2;
 		constexpr int NWD = sizeof(W) == 4 ? 8 : 16;
@@ -1815,81 +1887,67 @@ __global__ __launch_bounds__(128) void burst_wave_kernel(
 		__syncthreads();
 	const uint32_t lane = threadIdx.x & 63;
 	const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	const uint64_t i = blockIdx.x;
-	const uint64_t off = offsets[i];
-	uint32_t len = lens[i];
-	const uint8_t *p = base + off;
-	uint32_t st = PKT_OK, seq = 0, fl = 0;
-	const uint32_t (*lmid)[16] = mid;
-	if (MODE == HMAC_BURST_TX) {
-		seq = rx.seq[i];
-		fl = rx.flags[i];
-		const bool sg = (fl & PKT_PH_SIGNED) != 0;
-		const bool cr = (fl & PKT_PH_ENCRYPTED) != 0;
-		if (!sg || cr != (rx.enc_set != 0))
-			st = PKT_UNSAFE;
-		else if (len < 8 + dlen)
-			st = PKT_RESOURCE;	/* no room for header and hash */
-	} else {
-		if (len < 8) {
-			st = PKT_BAD;		/* header decode fails */
-		} else {
-			seq = load_be32_bytes(p);
-			fl = load_be32_bytes(p + 4);
-		}
-		/* net2_ck_rx_key (src/conn_keys.c:447-476) */
-		const bool use_alt = st == PKT_OK && rx.alt &&
-		    ((fl & PKT_PH_ALTKEY) != 0 || (!rx.no_cutoff &&
-		    seq - rx.rx_start >= rx.cutoff - rx.rx_start));
-		if (use_alt)
-			lmid = mid + 2;
-		const int enc_set = use_alt ? rx.alt_enc_set : rx.enc_set;
-		if (st == PKT_OK && ((fl & PKT_PH_SIGNED) == 0 ||
-		    (enc_set && (fl & PKT_PH_ENCRYPTED) == 0)))
-			st = PKT_UNSAFE;
-	}
-	const bool ok = st == PKT_OK;
-	/* the datagram's region after the header: hash field, then message */
-	const uint32_t rlen = ok ? len - 8 : 0;
-	const bool short_dgram = rlen < dlen;
-	const uint8_t *field = p + 8;
-	const uint8_t *m = field + dlen;
-	const uint32_t mlen = short_dgram ? 0 : rlen - dlen;
+	/* every lane of a wave works on datagram slot lane % G (the G slots
+	 * replicated across the wave: rounds on one lane of a wave run slower
+	 * than on all of them); lane d < G owns slot d's stores */
+	const uint32_t dl = lane % G;
+	const uint64_t i = (uint64_t)blockIdx.x * G + dl;
+	const bool live = i < n;
+	const bool mine = lane < G && live;	/* this lane stores datagram i */
+	BwDgram g = {};
+	if (live)
+		g = bw_decode<MODE, dlen>(base, offsets, lens, i, rx);
 
 	if (wv == 1) {
 		/* RX: the IV of an encrypted datagram that may verify */
-		if (MODE == HMAC_BURST_RX && ok && ivlen > 0 && iv != nullptr &&
-		    (fl & PKT_PH_ENCRYPTED) && lane == 0)
-			ph_iv_one(seq, fl, ivlen, reinterpret_cast<uint8_t *>(ivw));
+		if (MODE == HMAC_BURST_RX && mine && g.ok && ivlen > 0 &&
+		    iv != nullptr && (g.fl & PKT_PH_ENCRYPTED))
+			ph_iv_one(g.seq, g.fl, ivlen,
+			    reinterpret_cast<uint8_t *>(ivw[lane]));
 		__syncthreads();
 		return;
 	}
 
-	/* wave 0: HMAC of the message from the ipad midstate (a datagram
-	 * already refused, or without room for its hash field, hashes nothing) */
-	const bool hashed = ok && !short_dgram;
+	/* wave 0: HMAC of every owned message from its ipad midstate (a
+	 * datagram already refused, or without room for its hash field,
+	 * hashes nothing) */
+	const uint32_t nfull = g.mlen / H::BLOCK;
+	const uint32_t rem = g.mlen % H::BLOCK;
+	const uint32_t nb = !g.hashed ? 0 : nfull + 1 +
+	    (rem >= (uint32_t)(H::BLOCK - H::LENBYTES) ? 1 : 0);
+	if (lane < G) {
+		geo_m[lane] = g.off + 8 + dlen;
+		geo_len[lane] = g.mlen;
+		geo_nb[lane] = live ? nb : 0;
+	}
+	wave_lds_sync();
+	uint32_t nbmax = 0;
+	for (uint32_t d = 0; d < G; d++)
+		nbmax = max(nbmax, geo_nb[d]);
+	nbmax = __builtin_amdgcn_readfirstlane(nbmax);
+	const uint32_t K = BW_ROWS / G;
+	const uint32_t (*lmid)[16] = g.alt ? mid + 2 : mid;
 	typename H::State s;
 	load_mid<H>(lmid, 0, s);
-	const uint32_t nfull = mlen / H::BLOCK;
-	const uint32_t rem = mlen % H::BLOCK;
-	const uint32_t nb = !hashed ? 0 : nfull + 1 +
-	    (rem >= (uint32_t)(H::BLOCK - H::LENBYTES) ? 1 : 0);
-	const uint64_t bits = ((uint64_t)mlen + H::BLOCK) << 3;
-	for (uint32_t c0 = 0; c0 < nb; c0 += BW_NB) {
-		const uint32_t k = c0 + lane;
-		if (lane < BW_NB && k < nb) {
+	for (uint32_t c0 = 0; c0 < nbmax; c0 += K) {
+		/* row `lane`: block c0 + lane % K of datagram lane / K */
+		const uint32_t d = lane / K, k = c0 + lane % K;
+		if (d < G && k < geo_nb[d]) {
+			const uint32_t ml = geo_len[d];
 			uint32_t w[NW32];
-			bw_block<H>(m, k, nfull, rem, nb, bits, w);
+			bw_block<H>(base + geo_m[d], k, ml / H::BLOCK, ml % H::BLOCK,
+			    geo_nb[d], ((uint64_t)ml + H::BLOCK) << 3, w);
 			sched_row<H>(w, rows + lane * ROW);
 		}
 		wave_lds_sync();
-		const uint32_t cnt = min((uint32_t)BW_NB, nb - c0);
+		const uint32_t cnt = min(K, nbmax - c0);
 		for (uint32_t b = 0; b < cnt; b++)
-			rounds_row<H>(s, rows + b * ROW);
+			if (c0 + b < nb)
+				rounds_row<H>(s, rows + (dl * K + b) * ROW);
 		wave_lds_sync();
 	}
 	/* outer: one block = inner digest || 0x80 || 0... || bit count */
-	if (hashed) {
+	if (g.hashed) {
 		uint32_t w[NW32];
 #pragma unroll
 		for (int j = 0; j < NW32; j++)
@@ -1906,30 +1964,32 @@ __global__ __launch_bounds__(128) void burst_wave_kernel(
 		load_mid<H>(lmid, 1, s);
 		H::compress(s, w);
 	}
+	materialize<H>(s);
 	uint32_t o[16];
 	H::out_words(s, o, IS384);
-	__syncthreads();		/* wave 1's IV is in LDS */
-	if (lane != 0)
+	__syncthreads();		/* wave 1's IVs are in LDS */
+	if (!mine)
 		return;
+	const uint8_t *field = base + g.off + 8;
 	if (MODE == HMAC_BURST_RX) {
-		uint32_t code = st;
-		if (ok) {		/* net2_buffer_cmp, packet.n2t:253-257 */
+		uint32_t code = g.st;
+		if (g.ok) {		/* net2_buffer_cmp, packet.n2t:253-257 */
 			uint32_t diff = 0;
-			if (hashed) {
+			if (g.hashed) {
 #pragma unroll
 				for (uint32_t j = 0; j < dlen; j++)
 					diff |= field[j] ^
 					    ((o[j >> 2] >> (8 * (j & 3))) & 0xffu);
 			}
-			code = !hashed || diff != 0 ? PKT_BAD : PKT_OK;
+			code = !g.hashed || diff != 0 ? PKT_BAD : PKT_OK;
 		}
 		if (rx.seq != nullptr) {
-			rx.seq[i] = seq;
-			rx.flags[i] = fl;
+			rx.seq[i] = g.seq;
+			rx.flags[i] = g.fl;
 		}
 		if (code == PKT_OK && ivlen > 0 && iv != nullptr &&
-		    (fl & PKT_PH_ENCRYPTED)) {
-			const uint8_t *src = reinterpret_cast<const uint8_t *>(ivw);
+		    (g.fl & PKT_PH_ENCRYPTED)) {
+			const uint8_t *src = reinterpret_cast<const uint8_t *>(ivw[lane]);
 			uint8_t *dst = iv + i * ivlen;
 			for (uint32_t b = 0; b < ivlen; b++)
 				dst[b] = src[b];
@@ -1940,22 +2000,23 @@ __global__ __launch_bounds__(128) void burst_wave_kernel(
 	/* TX */
 	if (rx.rec != nullptr) {
 		uint8_t *r = rx.rec + i * (dlen + 16);
-		if (hashed)
+		if (g.hashed)
 			store_digest<dlen>(r, o);
 		*reinterpret_cast<uint4 *>(r + dlen) = make_uint4(
-		    ok ? bswap32(seq) : 0u, ok ? bswap32(fl) : 0u, (uint32_t)i, st);
+		    g.ok ? bswap32(g.seq) : 0u, g.ok ? bswap32(g.fl) : 0u,
+		    (uint32_t)i, g.st);
 		return;
 	}
-	if (hashed) {
-		uint8_t *h = out + off;
+	if (g.hashed) {
+		uint8_t *h = out + g.off;
 #pragma unroll
 		for (int b = 0; b < 4; b++) {
-			h[b] = (uint8_t)(seq >> (24 - 8 * b));
-			h[4 + b] = (uint8_t)(fl >> (24 - 8 * b));
+			h[b] = (uint8_t)(g.seq >> (24 - 8 * b));
+			h[4 + b] = (uint8_t)(g.fl >> (24 - 8 * b));
 		}
 		store_digest<dlen>(h + 8, o);
 	}
-	result[i] = (uint8_t)st;
+	result[i] = (uint8_t)g.st;
 }
 
 /* ---- length binning (counting sort by block count, longest first) ---- */
@@ -2822,27 +2883,23 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 	return hipGetLastError();
 }
 template <class H, bool IS384>
-static void launch_burst_wave(int mode, uint64_t n, hipStream_t s,
+static void launch_burst_wave(int mode, uint64_t n, uint32_t G, hipStream_t s,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
     const HMid &hm, const BurstArgs &a, uint8_t *result, uint8_t *iv,
     uint32_t ivlen, uint8_t *out)
 {
+	const unsigned grid = (unsigned)((n + G - 1) / G);
 	if (mode == HMAC_BURST_RX)
-		burst_wave_kernel<H, HMAC_BURST_RX, IS384><<<(unsigned)n, 128, 0, s>>>(
-		    base, offsets, lens, hm, a, result, iv, ivlen, out);
+		burst_wave_kernel<H, HMAC_BURST_RX, IS384><<<grid, 128, 0, s>>>(
+		    base, offsets, lens, n, G, hm, a, result, iv, ivlen, out);
 	else
-		burst_wave_kernel<H, HMAC_BURST_TX, IS384><<<(unsigned)n, 128, 0, s>>>(
-		    base, offsets, lens, hm, a, result, iv, ivlen, out);
+		burst_wave_kernel<H, HMAC_BURST_TX, IS384><<<grid, 128, 0, s>>>(
+		    base, offsets, lens, n, G, hm, a, result, iv, ivlen, out);
 }
 
-uint64_t net2_burst_wave_max(void)
+/* SIMDs of the current device (0: unknown), cached per ordinal. */
+static uint64_t device_simds()
 {
-	/* read per call (a test compares both forms in one process) */
-	const char *e = getenv("NET2_BURST_WAVE_MAX");
-	if (e != nullptr && *e != '\0')
-		return strtoull(e, nullptr, 10);
-	/* one datagram per SIMD: beyond that the wave form's datagrams share
-	 * SIMDs while the lane form's latency does not grow until ~64x more */
 	static std::atomic<int> cus[64];
 	int dev = 0;
 	if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
@@ -2861,13 +2918,24 @@ uint64_t net2_burst_wave_max(void)
 	return (uint64_t)c * 4;
 }
 
+uint64_t net2_burst_wave_max(void)
+{
+	/* read per call (a test compares both forms in one process) */
+	const char *e = getenv("NET2_BURST_WAVE_MAX");
+	if (e != nullptr && *e != '\0')
+		return strtoull(e, nullptr, 10);
+	/* BW_GMAX datagrams per SIMD: beyond that a pass of the wave form
+	 * expands too few blocks per datagram to beat the lane form */
+	return device_simds() * BW_GMAX;
+}
+
 hipError_t net2_launch_burst_wave(int alg, const uint8_t *key, size_t keylen,
     const uint8_t *base, const uint64_t *offsets, const uint32_t *lens,
     uint64_t n, const BurstArgs *args, uint8_t *result, uint8_t *iv,
     uint32_t ivlen, uint8_t *out, int mode, hipStream_t s)
 {
 	if ((mode != HMAC_BURST_RX && mode != HMAC_BURST_TX) || args == nullptr ||
-	    offsets == nullptr || ivlen > 64 || n > 0x7fffffffu)
+	    offsets == nullptr || ivlen > 64 || n > 0xffffffffu)
 		return hipErrorInvalidValue;
 	if (mode == HMAC_BURST_RX && args->rec != nullptr)
 		return hipErrorInvalidValue;
@@ -2890,15 +2958,19 @@ hipError_t net2_launch_burst_wave(int alg, const uint8_t *key, size_t keylen,
 				ab[4 * j + b] = (uint8_t)(args->altkey[j] >> (24 - 8 * b));
 		hmac_midstates(halg, ab, &hm, 2);
 	}
+	/* datagrams per workgroup: about one workgroup per SIMD */
+	const uint64_t simds = std::max<uint64_t>(device_simds(), 1);
+	const uint32_t G = (uint32_t)std::min<uint64_t>(BW_GMAX,
+	    std::max<uint64_t>(1, (n + simds - 1) / simds));
 	if (halg == NET2_ALG_SHA256)
-		launch_burst_wave<Sha256H, false>(mode, n, s, base, offsets, lens,
-		    hm, *args, result, iv, ivlen, out);
+		launch_burst_wave<Sha256H, false>(mode, n, G, s, base, offsets,
+		    lens, hm, *args, result, iv, ivlen, out);
 	else if (halg == NET2_ALG_SHA384)
-		launch_burst_wave<Sha512H, true>(mode, n, s, base, offsets, lens,
-		    hm, *args, result, iv, ivlen, out);
+		launch_burst_wave<Sha512H, true>(mode, n, G, s, base, offsets,
+		    lens, hm, *args, result, iv, ivlen, out);
 	else
-		launch_burst_wave<Sha512H, false>(mode, n, s, base, offsets, lens,
-		    hm, *args, result, iv, ivlen, out);
+		launch_burst_wave<Sha512H, false>(mode, n, G, s, base, offsets,
+		    lens, hm, *args, result, iv, ivlen, out);
 	return hipGetLastError();
 }
 

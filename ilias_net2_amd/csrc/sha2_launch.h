@@ -131,8 +131,8 @@ hipError_t net2_launch_hmac(int alg, const uint8_t *key, size_t keylen,
 
 /*
  * Small keyed bursts (net2_packet_{decode,encode}_burst with a hash key, at
- * most net2_burst_wave_max() datagrams): one workgroup per datagram
- * (burst_wave_kernel) instead of one lane -- the burst's time is one
+ * most net2_burst_wave_max() datagrams): 1 to 16 datagrams per workgroup
+ * (burst_wave_kernel) instead of 64 per wave -- the burst's time is one
  * datagram's chain either way, and the wave form shortens it by expanding
  * the message schedules in parallel.  mode NET2_HMAC_MODE_BURST_RX / _TX;
  * args as for net2_launch_hmac (RX: seq / flags receive the decoded headers,
@@ -146,7 +146,7 @@ hipError_t net2_launch_burst_wave(int alg, const uint8_t *key, size_t keylen,
     uint64_t n, const BurstArgs *args, uint8_t *result, uint8_t *iv,
     uint32_t ivlen, uint8_t *out, int mode, hipStream_t s);
 /* The largest burst net2_launch_burst_wave is for on the current device:
- * one datagram per SIMD (NET2_BURST_WAVE_MAX overrides; 0: never). */
+ * 16 datagrams per SIMD (NET2_BURST_WAVE_MAX overrides; 0: never). */
 uint64_t net2_burst_wave_max(void);
 
 /*

@@ -1771,8 +1771,8 @@ int decode_burst(const struct net2_burst_rx_keys *k, uint32_t ivlen,
 				rx.altkey[i / 4] |= (uint32_t)ak[i] << (24 - 8 * (i % 4));
 		}
 		if (n <= net2_burst_wave_max()) {
-			/* a small burst: one workgroup per datagram, codes,
-			 * headers and IVs stored by that one launch */
+			/* a small burst: 1 to 16 datagrams per workgroup,
+			 * codes, headers and IVs stored by that one launch */
 			rx.seq = d_seq;
 			rx.flags = d_flags;
 			rx.status = nullptr;
@@ -1824,7 +1824,7 @@ int encode_burst(int hash_alg, const void *hash_key, size_t hash_keylen,
 		tx.enc_set = enc_alg != 0;
 		tx.rec = rec;
 		if (n <= net2_burst_wave_max()) {
-			/* a small burst: one workgroup per datagram */
+			/* a small burst: 1 to 16 datagrams per workgroup */
 			HIP_TRY(net2_launch_burst_wave(hash_alg,
 			    (const uint8_t *)hash_key, hash_keylen,
 			    (const uint8_t *)d_base, d_offsets, d_lens, n, &tx,

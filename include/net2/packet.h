@@ -60,10 +60,10 @@ int net2_ph_to_iv_dev(const uint32_t *d_seq, const uint32_t *d_flags,
  * length-binning area comes first, at the same place for every n: one
  * workspace serves bursts of any size up to its own, and
  * net2_sha2_workspace_init / net2_sha2_workspace_stats (net2/sha2_batch.h)
- * prepare and inspect it.  A keyed burst of at most one datagram per SIMD
- * of the device (1,024 on an MI355X; NET2_BURST_WAVE_MAX overrides) is
- * hashed one workgroup per datagram, in one launch, without touching the
- * workspace; a larger one below NET2_BURST_BIN_MIN datagrams (default
+ * prepare and inspect it.  A keyed burst of at most 16 datagrams per SIMD
+ * of the device (16,384 on an MI355X; NET2_BURST_WAVE_MAX overrides) is
+ * hashed 1 to 16 datagrams per workgroup, in one launch, without touching
+ * the workspace; a larger one below NET2_BURST_BIN_MIN datagrams (default
  * 65,536: at most one wave per SIMD) is hashed in arrival order, without
  * the binning launch.
  */

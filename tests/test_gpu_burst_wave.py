@@ -1,8 +1,8 @@
-"""The wave form of the keyed packet bursts (burst_wave_kernel: one
-workgroup per datagram, the message schedules expanded by the wave's lanes,
+"""The wave form of the keyed packet bursts (burst_wave_kernel: 1 to 16
+datagrams per workgroup, the message schedules expanded by the wave's lanes,
 codes / headers / IVs stored by the one launch), which
-net2_packet_{decode,encode}_burst[_host] take for bursts of at most one
-datagram per SIMD (net2_burst_wave_max).
+net2_packet_{decode,encode}_burst[_host] take for bursts of at most 16
+datagrams per SIMD (net2_burst_wave_max).
 
 Every parity test of the lane form is run again in the wave form
 (NET2_BURST_WAVE_MAX raised so bursts of any size take it): the
@@ -10,7 +10,8 @@ device-resident bursts of tests/test_gpu_packet.py (six key set-ups, mixed
 and wrong flags, slots without room, runts, tampered bytes, the alternate rx
 key of net2_ck_rx_key), and the host bursts of tests/test_gpu_burst_host.py
 (sliced over 1 and 3 devices, key rollover, pinned layouts, datagrams up to
-the UDP maximum -- 512 SHA-512 blocks, 32 passes of the 16-row schedule).
+the UDP maximum -- 512 SHA-512 blocks, 128 passes of 4 blocks at 12
+datagrams per workgroup).
 Then the default threshold itself at integration-sized bursts, and the two
 forms against each other byte for byte.
 """
@@ -109,8 +110,9 @@ def _burst(n, seed, hash_alg, enc_set):
 def test_small_host_bursts_default_threshold(dev, oracle_mod, n, hash_alg, enc_set,
                                              ivlen):
     """Integration-sized bursts at the default threshold (the wave form up
-    to one datagram per SIMD, the lane form above, unbinned below 65,536
-    datagrams): TX, then RX with tampered bytes and runts,
+    to 16 datagrams per SIMD -- 1, 2, 5 and 16 datagrams per workgroup
+    here -- the lane form above, unbinned below 65,536 datagrams): TX, then
+    RX with tampered bytes and runts,
     pinned and pageable buffers, every code / sealed byte / header / IV
     against the oracle.  Message lengths straddle the padding boundaries
     (55/56, 111/112, 119/120 bytes: the length field in the tail block or a
