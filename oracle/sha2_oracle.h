@@ -104,9 +104,6 @@ int oracle_hmac_digest(int alg, const uint8_t *key, size_t keylen,
  */
 int oracle_ph_to_iv(uint32_t seq, uint32_t flags, size_t ivlen, uint8_t *iv);
 
-#ifdef __cplusplus
-}
-#endif
 /*
  * Threaded batch forms (each item independent), so full-size GPU tests
  * check every result against the oracle.  HMAC over a batch under one key
@@ -133,4 +130,7 @@ int oracle_packet_encode_batch(int hash_alg, const uint8_t *key,
     uint8_t *base, const uint64_t *offsets, const uint32_t *lens, size_t n,
     uint8_t *result, int nthreads);
 
+#ifdef __cplusplus
+}
+#endif
 #endif /* NET2_SHA2_ORACLE_H */
