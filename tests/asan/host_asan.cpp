@@ -201,7 +201,9 @@ static void single_calls()
 				s = s * 6364136223846793005ull + 1442695040888963407ull;
 				const int alg = 1 + (int)((s >> 33) % 6);	/* 1..3, HMAC 4..6 */
 				const size_t len = (size_t)((s >> 20) % 3000);
-				std::vector<uint8_t> m(len + 1), key(37);
+				/* an HMAC row takes a key of its registry length */
+				std::vector<uint8_t> m(len + 1),
+				    key(alg > 3 ? (size_t)net2_hash_getkeylen(alg) : 1);
 				for (size_t i = 0; i < len; i++)
 					m[i] = (uint8_t)(s >> (i % 56));
 				for (size_t i = 0; i < key.size(); i++)
