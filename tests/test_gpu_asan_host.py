@@ -10,6 +10,8 @@ free or a leak in our host code aborts it; leaks the HIP / HSA runtimes keep
 until exit are suppressed (tests/asan/lsan.supp).  Run once on the real
 device count and once with three virtual devices, so the sharded paths
 (one slice per device, persistent slice workers) run under ASan too.
+`tests/asan/test_sign_asan` does the same for the host C layer of the
+signed-payload callers (csrc/host/*.c) through tests/c/test_sign.c.
 """
 import os
 import subprocess
@@ -18,6 +20,19 @@ import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 EXE = os.path.join(HERE, "asan", "host_asan")
+SIGN = os.path.join(HERE, "asan", "test_sign_asan")
+KEYS = [os.path.join(HERE, "golden", "keys", f)
+        for f in ("ecdsa_p521_priv.pem", "ecdsa_p521_pub.pem")]
+
+
+def _env(virtual=None):
+    env = dict(os.environ)
+    env["ASAN_OPTIONS"] = "detect_leaks=1:abort_on_error=0:halt_on_error=1"
+    env["LSAN_OPTIONS"] = "suppressions=" + os.path.join(HERE, "asan", "lsan.supp")
+    env.pop("NET2_SHA2_VIRTUAL_DEVICES", None)
+    if virtual:
+        env["NET2_SHA2_VIRTUAL_DEVICES"] = virtual
+    return env
 
 
 @pytest.mark.gpu
@@ -25,15 +40,27 @@ EXE = os.path.join(HERE, "asan", "host_asan")
 def test_host_code_under_asan(virtual):
     if not os.path.exists(EXE):
         pytest.skip("tests/asan/host_asan not built (make -C tests/asan)")
-    env = dict(os.environ)
-    env["ASAN_OPTIONS"] = "detect_leaks=1:abort_on_error=0:halt_on_error=1"
-    env["LSAN_OPTIONS"] = "suppressions=" + os.path.join(HERE, "asan", "lsan.supp")
-    env.pop("NET2_SHA2_VIRTUAL_DEVICES", None)
-    if virtual:
-        env["NET2_SHA2_VIRTUAL_DEVICES"] = virtual
-    run = subprocess.run([EXE], capture_output=True, text=True, env=env, timeout=300)
+    run = subprocess.run([EXE], capture_output=True, text=True, env=_env(virtual),
+                         timeout=300)
     out = run.stdout + run.stderr
     print(out[-3000:])
     assert run.returncode == 0, out[-6000:]
     assert "host_asan ok" in run.stdout
+    assert "AddressSanitizer" not in out and "LeakSanitizer" not in out
+
+
+@pytest.mark.gpu
+def test_signed_payload_layer_under_asan():
+    """tests/c/test_sign.c (the reference's test/sign.c restated, parts 1-3:
+    fingerprints, signature create / validate single and batched, the
+    signed-carver tick at 4096 x 1 KiB with its helper pool) over the host C
+    layer and the library, both built with ASan."""
+    if not os.path.exists(SIGN):
+        pytest.skip("tests/asan/test_sign_asan not built (make -C tests/asan)")
+    run = subprocess.run([SIGN, *KEYS], capture_output=True, text=True, env=_env(),
+                         timeout=300)
+    out = run.stdout + run.stderr
+    print(out[-3000:])
+    assert run.returncode == 0, out[-6000:]
+    assert "PASS (0 failures)" in run.stdout
     assert "AddressSanitizer" not in out and "LeakSanitizer" not in out
