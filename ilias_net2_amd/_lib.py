@@ -78,6 +78,7 @@ SIGNATURES = {
     "net2_sha2_workspace_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t,
                                                  ctypes.c_void_p]),
     "net2_sha2_bin_limits": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_int64]),
+    "net2_sha2_burst_limits": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64]),
     "net2_sha2_batch": (ctypes.c_int, [
         ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
         ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,

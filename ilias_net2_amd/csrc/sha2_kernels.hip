@@ -2918,12 +2918,27 @@ static uint64_t device_simds()
 	return (uint64_t)c * 4;
 }
 
+/* net2_sha2_burst_limits' setting (-1: none) */
+static std::atomic<int64_t> g_burst_wave_max{-1};
+
+void net2_set_burst_wave_max(int64_t v)
+{
+	g_burst_wave_max.store(v < 0 ? -1 : v, std::memory_order_relaxed);
+}
+
 uint64_t net2_burst_wave_max(void)
 {
-	/* read per call (a test compares both forms in one process) */
-	const char *e = getenv("NET2_BURST_WAVE_MAX");
-	if (e != nullptr && *e != '\0')
-		return strtoull(e, nullptr, 10);
+	const int64_t set = g_burst_wave_max.load(std::memory_order_relaxed);
+	if (set >= 0)
+		return (uint64_t)set;
+	/* NET2_BURST_WAVE_MAX, read once (A/B runs, one process per setting) */
+	static const int64_t env = [] {
+		const char *e = getenv("NET2_BURST_WAVE_MAX");
+		return e != nullptr && *e != '\0' ?
+		    (int64_t)(strtoull(e, nullptr, 10) & INT64_MAX) : (int64_t)-1;
+	}();
+	if (env >= 0)
+		return (uint64_t)env;
 	/* BW_GMAX datagrams per SIMD: beyond that a pass of the wave form
 	 * expands too few blocks per datagram to beat the lane form */
 	return device_simds() * BW_GMAX;

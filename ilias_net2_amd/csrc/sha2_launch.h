@@ -146,8 +146,11 @@ hipError_t net2_launch_burst_wave(int alg, const uint8_t *key, size_t keylen,
     uint64_t n, const BurstArgs *args, uint8_t *result, uint8_t *iv,
     uint32_t ivlen, uint8_t *out, int mode, hipStream_t s);
 /* The largest burst net2_launch_burst_wave is for on the current device:
- * 16 datagrams per SIMD (NET2_BURST_WAVE_MAX overrides; 0: never). */
+ * 16 datagrams per SIMD, unless net2_sha2_burst_limits set a limit
+ * (net2_set_burst_wave_max; < 0 clears it) or NET2_BURST_WAVE_MAX was in
+ * the environment at first use (0: never). */
 uint64_t net2_burst_wave_max(void);
+void net2_set_burst_wave_max(int64_t v);
 
 /*
  * Coalesced small jobs (sha2_coalesce.cpp): many independent requests from

@@ -1718,19 +1718,31 @@ int check_burst_args(int hash_alg, const void *key, size_t keylen,
 	return check_current_device();
 }
 
+/* net2_sha2_burst_limits' binning threshold (-1: none) */
+std::atomic<int64_t> g_burst_bin_min{-1};
+
 /*
- * The binning workspace a burst's HMAC kernel is given: below
- * NET2_BURST_BIN_MIN datagrams (default 65,536: one lane per datagram, one
- * wave per SIMD) none -- every wave then has a SIMD of its own, the burst
- * takes its longest wave's time whatever the order, and the binning launch
- * is pure fixed cost (tools/burst_sizes.py).  Read per call.
+ * The binning workspace a burst's HMAC kernel is given: below the binning
+ * threshold (default 65,536 datagrams: one lane per datagram, one wave per
+ * SIMD) none -- every wave then has a SIMD of its own, the burst takes its
+ * longest wave's time whatever the order, and the binning launch is pure
+ * fixed cost (tools/burst_sizes.py).  The threshold is
+ * net2_sha2_burst_limits' setting, else NET2_BURST_BIN_MIN from the
+ * environment at first use (A/B runs), else the default.
  */
 uint32_t *burst_bins(uint64_t n, uint32_t *bin)
 {
-	const char *e = getenv("NET2_BURST_BIN_MIN");
-	const uint64_t min_n = e != nullptr && *e != '\0' ?
-	    strtoull(e, nullptr, 10) : (uint64_t)65536;
-	return n >= min_n ? bin : nullptr;
+	int64_t min_n = g_burst_bin_min.load(std::memory_order_relaxed);
+	if (min_n < 0) {
+		static const int64_t env = [] {
+			const char *e = getenv("NET2_BURST_BIN_MIN");
+			return e != nullptr && *e != '\0' ?
+			    (int64_t)(strtoull(e, nullptr, 10) & INT64_MAX) :
+			    (int64_t)65536;
+		}();
+		min_n = env;
+	}
+	return n >= (uint64_t)min_n ? bin : nullptr;
 }
 
 /*
@@ -1854,6 +1866,13 @@ int encode_burst(int hash_alg, const void *hash_key, size_t hash_keylen,
 NET2_EXPORT size_t net2_packet_burst_workspace(uint64_t n)
 {
 	return burst_layout(n, nullptr, nullptr);
+}
+
+NET2_EXPORT int net2_sha2_burst_limits(int64_t wave_max, int64_t bin_min)
+{
+	net2_set_burst_wave_max(wave_max);
+	g_burst_bin_min.store(bin_min < 0 ? -1 : bin_min, std::memory_order_relaxed);
+	return 0;
 }
 
 NET2_EXPORT int net2_packet_decode_burst_ck(const struct net2_burst_rx_keys *k,

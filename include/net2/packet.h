@@ -61,13 +61,23 @@ int net2_ph_to_iv_dev(const uint32_t *d_seq, const uint32_t *d_flags,
  * workspace serves bursts of any size up to its own, and
  * net2_sha2_workspace_init / net2_sha2_workspace_stats (net2/sha2_batch.h)
  * prepare and inspect it.  A keyed burst of at most 16 datagrams per SIMD
- * of the device (16,384 on an MI355X; NET2_BURST_WAVE_MAX overrides) is
- * hashed 1 to 16 datagrams per workgroup, in one launch, without touching
- * the workspace; a larger one below NET2_BURST_BIN_MIN datagrams (default
- * 65,536: at most one wave per SIMD) is hashed in arrival order, without
- * the binning launch.
+ * of the device (16,384 on an MI355X) is hashed 1 to 16 datagrams per
+ * workgroup, in one launch, without touching the workspace; a larger one
+ * below 65,536 datagrams (at most one wave per SIMD) is hashed in arrival
+ * order, without the binning launch (net2_sha2_burst_limits below).
  */
 size_t net2_packet_burst_workspace(uint64_t n);
+
+/*
+ * Size thresholds of the keyed bursts, process-wide (diagnostics, tests and
+ * A/B runs): wave_max is the largest burst hashed by the one-launch
+ * small-burst form (0: never), bin_min the smallest burst whose datagrams
+ * are length-binned first.  A value < 0 restores that threshold's default
+ * (16 datagrams per SIMD / 65,536, or NET2_BURST_WAVE_MAX /
+ * NET2_BURST_BIN_MIN when set in the environment at first use).  Results do
+ * not depend on either; only the time does.  Always 0.
+ */
+int net2_sha2_burst_limits(int64_t wave_max, int64_t bin_min);
 
 /*
  * RX: the hash steps of net2_packet_decode for a burst of n received

@@ -5,7 +5,7 @@ net2_packet_{decode,encode}_burst[_host] take for bursts of at most 16
 datagrams per SIMD (net2_burst_wave_max).
 
 Every parity test of the lane form is run again in the wave form
-(NET2_BURST_WAVE_MAX raised so bursts of any size take it): the
+(net2_sha2_burst_limits raises the limit so bursts of any size take it): the
 device-resident bursts of tests/test_gpu_packet.py (six key set-ups, mixed
 and wrong flags, slots without room, runts, tampered bytes, the alternate rx
 key of net2_ck_rx_key), and the host bursts of tests/test_gpu_burst_host.py
@@ -40,9 +40,13 @@ def dev():
 
 
 @pytest.fixture
-def wave(monkeypatch):
+def wave():
     """Every keyed burst of the test in the wave form."""
-    monkeypatch.setenv("NET2_BURST_WAVE_MAX", str(1 << 30))
+    from ilias_net2_amd import _lib
+    L = _lib.lib()
+    assert L.net2_sha2_burst_limits(1 << 30, -1) == 0
+    yield
+    L.net2_sha2_burst_limits(-1, -1)
 
 
 @pytest.fixture
@@ -150,9 +154,9 @@ def test_small_host_bursts_default_threshold(dev, oracle_mod, n, hash_alg, enc_s
         H.check_decode(got, want, ivlen)
 
 
-def test_wave_and_lane_forms_agree(dev, monkeypatch, oracle_mod):
+def test_wave_and_lane_forms_agree(dev, oracle_mod):
     """One device-resident burst of 1,000 datagrams decoded in both forms
-    (NET2_BURST_WAVE_MAX 0: lane form; default: wave form): codes, decoded
+    (net2_sha2_burst_limits wave_max 0: lane form; default: wave form): codes, decoded
     headers and the whole IV array -- rows left untouched included --
     identical, and equal to the oracle."""
     from ilias_net2_amd import _lib
@@ -168,11 +172,8 @@ def test_wave_and_lane_forms_agree(dev, monkeypatch, oracle_mod):
     ws = torch.empty(L.net2_packet_burst_workspace(n), dtype=torch.uint8, device=dev)
     st = torch.cuda.current_stream().cuda_stream
     outs = []
-    for form in ("0", None):
-        if form is None:
-            monkeypatch.delenv("NET2_BURST_WAVE_MAX", raising=False)
-        else:
-            monkeypatch.setenv("NET2_BURST_WAVE_MAX", form)
+    for wave_max in (0, -1):          # lane form, then the default (wave form)
+        assert L.net2_sha2_burst_limits(wave_max, -1) == 0
         res = torch.full((n,), 9, dtype=torch.uint8, device=dev)
         iv = torch.full((n, ivlen), 0x5a, dtype=torch.uint8, device=dev)
         oseq = torch.full((n,), 7, dtype=torch.int32, device=dev)
