@@ -1816,12 +1816,15 @@ int decode_burst(const struct net2_burst_rx_keys *k, uint32_t ivlen,
 /*
  * The hash steps of net2_packet_encode for a device-resident burst.  rec
  * (keyed hash only): header and hash field of every datagram to a record of
- * their own (BurstArgs::rec) instead of into d_base.
+ * their own (BurstArgs::rec) instead of into d_base.  bin: length-bin the
+ * burst at or above the threshold (burst_bins); the host path passes false
+ * where the order of the records matters more than the kernel's time.
  */
 int encode_burst(int hash_alg, const void *hash_key, size_t hash_keylen,
     int enc_alg, const uint32_t *d_seq, const uint32_t *d_flags,
     void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
-    uint64_t n, uint8_t *d_result, void *d_ws, hipStream_t s, uint8_t *rec)
+    uint64_t n, uint8_t *d_result, void *d_ws, hipStream_t s, uint8_t *rec,
+    bool bin = true)
 {
 	BurstWs w;
 	burst_layout(n, (uint8_t *)d_ws, &w);
@@ -1847,8 +1850,8 @@ int encode_burst(int hash_alg, const void *hash_key, size_t hash_keylen,
 		}
 		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)hash_key,
 		    hash_keylen, (const uint8_t *)d_base, d_offsets, d_lens, 0,
-		    0, n, (uint8_t *)d_base, burst_bins(n, w.bin), s,
-		    NET2_HMAC_MODE_BURST_TX, &tx));
+		    0, n, (uint8_t *)d_base, bin ? burst_bins(n, w.bin) : nullptr,
+		    s, NET2_HMAC_MODE_BURST_TX, &tx));
 		FI_POINT(FI_KERNEL);
 		return 0;
 	}
@@ -2213,9 +2216,22 @@ int enqueue_burst_steps(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 			(void)hipGetLastError();
 			return EIO;
 		}
+		/*
+		 * Datagrams copied as they lie (page-locked input) are hashed in
+		 * arrival order: the records then come back in the order of the
+		 * caller's buffer, and the scatter of sealed headers below
+		 * writes it front to back instead of in length order -- 64 K
+		 * MTU datagrams 1.23 against 1.28-1.30 ms, 1 M 0.9 % faster
+		 * (profiles/round6/txbin*_*.jsonl), while the unbinned kernel
+		 * stays hidden under the next chunk's copy.  Packed (pageable)
+		 * input keeps the binning: there the pack of the next chunk
+		 * shares the host threads with the scatter, and with no binning
+		 * at all it measured 1.5 % slower (binoff_*.jsonl, DESIGN.md
+		 * 6.4).
+		 */
 		if ((rc = encode_burst(hb.hash_alg, hb.hash_key, hb.hash_keylen,
 		    hb.enc_alg, dm.hdr, dm.hdr + n, s.d_in, dm.off, dm.len, n,
-		    k_res, s.d_ws, s.stream, (uint8_t *)recd)) != 0)
+		    k_res, s.d_ws, s.stream, (uint8_t *)recd, !direct)) != 0)
 			return rc;
 	}
 	FI_POINT(FI_RECORD);
