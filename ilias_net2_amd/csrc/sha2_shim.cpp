@@ -1824,8 +1824,12 @@ int encode_burst(int hash_alg, const void *hash_key, size_t hash_keylen,
     int enc_alg, const uint32_t *d_seq, const uint32_t *d_flags,
     void *d_base, const uint64_t *d_offsets, const uint32_t *d_lens,
     uint64_t n, uint8_t *d_result, void *d_ws, hipStream_t s, uint8_t *rec,
-    bool bin = true)
+    bool bin = true, uint8_t *seal_to = nullptr)
 {
+	/* seal_to (keyed, no rec): headers and hash fields go there, at the
+	 * datagrams' offsets, instead of into d_base (the host path: the
+	 * caller's page-locked buffer through its device mapping) */
+	uint8_t *const out = seal_to != nullptr ? seal_to : (uint8_t *)d_base;
 	BurstWs w;
 	burst_layout(n, (uint8_t *)d_ws, &w);
 	if (hash_alg != NET2_HASH_NIL) {
@@ -1843,15 +1847,14 @@ int encode_burst(int hash_alg, const void *hash_key, size_t hash_keylen,
 			HIP_TRY(net2_launch_burst_wave(hash_alg,
 			    (const uint8_t *)hash_key, hash_keylen,
 			    (const uint8_t *)d_base, d_offsets, d_lens, n, &tx,
-			    d_result, nullptr, 0, (uint8_t *)d_base,
-			    NET2_HMAC_MODE_BURST_TX, s));
+			    d_result, nullptr, 0, out, NET2_HMAC_MODE_BURST_TX, s));
 			FI_POINT(FI_KERNEL);
 			return 0;
 		}
 		HIP_TRY(net2_launch_hmac(hash_alg, (const uint8_t *)hash_key,
 		    hash_keylen, (const uint8_t *)d_base, d_offsets, d_lens, 0,
-		    0, n, (uint8_t *)d_base, bin ? burst_bins(n, w.bin) : nullptr,
-		    s, NET2_HMAC_MODE_BURST_TX, &tx));
+		    0, n, out, bin ? burst_bins(n, w.bin) : nullptr, s,
+		    NET2_HMAC_MODE_BURST_TX, &tx));
 		FI_POINT(FI_KERNEL);
 		return 0;
 	}
@@ -2180,6 +2183,7 @@ int enqueue_burst_steps(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 	if (k_res == nullptr)
 		return EIO;
 	std::vector<std::function<void()>> copies;
+	bool sealed = false;	/* TX sealed in place by the kernel */
 	if (!hb.tx) {
 		const uint32_t ivlen = hb.keys->enc_alg != 0 ? hb.ivlen : 0;
 		uint8_t *st_iv = st_b;
@@ -2210,35 +2214,53 @@ int enqueue_burst_steps(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 			    (size_t)n * 4); });
 	} else {
 		const bool keyed = hb.hash_alg != NET2_HASH_NIL;
-		void *recd = nullptr;
-		if (keyed && (hipHostGetDevicePointer(&recd, st_b, 0) != hipSuccess ||
+		/*
+		 * Datagrams copied as they lie from one page-locked allocation:
+		 * the kernel seals headers and hash fields straight into the
+		 * caller's buffer through its mapping (no records, no host
+		 * scatter).  Otherwise it fills one record per datagram in the
+		 * slot's mapped staging, scattered by the host when the chunk is
+		 * done.
+		 */
+		void *recd = nullptr, *seal = nullptr;
+		if (keyed && direct && (hipHostGetDevicePointer(&seal, hb.base + rs,
+		    0) != hipSuccess || seal == nullptr)) {
+			(void)hipGetLastError();
+			seal = nullptr;
+		}
+		if (keyed && seal == nullptr &&
+		    (hipHostGetDevicePointer(&recd, st_b, 0) != hipSuccess ||
 		    recd == nullptr)) {
 			(void)hipGetLastError();
 			return EIO;
 		}
 		/*
 		 * Datagrams copied as they lie (page-locked input) are hashed in
-		 * arrival order: the records then come back in the order of the
-		 * caller's buffer, and the scatter of sealed headers below
-		 * writes it front to back instead of in length order -- 64 K
-		 * MTU datagrams 1.23 against 1.28-1.30 ms, 1 M 0.9 % faster
-		 * (profiles/round6/txbin*_*.jsonl), while the unbinned kernel
-		 * stays hidden under the next chunk's copy.  Packed (pageable)
-		 * input keeps the binning: there the pack of the next chunk
-		 * shares the host threads with the scatter, and with no binning
-		 * at all it measured 1.5 % slower (binoff_*.jsonl, DESIGN.md
-		 * 6.4).
+		 * arrival order and sealed in place by the kernel: TX from
+		 * pinned memory 2-7 % faster from 1,024 to 16,384 datagrams
+		 * than records scattered by the host, the same at 1 M
+		 * (profiles/round6/seal_*.jsonl).  Before the kernel sealed
+		 * them, arrival order already won over the binned order by
+		 * letting the host scatter walk the buffer front to back
+		 * (txbin*_*.jsonl); the unbinned kernel stays hidden under the
+		 * next chunk's copy.  Packed (pageable) input keeps the binning
+		 * and the records: there the pack of the next chunk shares the
+		 * host threads with the scatter, and with no binning at all it
+		 * measured 1.5 % slower (binoff_*.jsonl).
 		 */
 		if ((rc = encode_burst(hb.hash_alg, hb.hash_key, hb.hash_keylen,
 		    hb.enc_alg, dm.hdr, dm.hdr + n, s.d_in, dm.off, dm.len, n,
-		    k_res, s.d_ws, s.stream, (uint8_t *)recd, !direct)) != 0)
+		    k_res, s.d_ws, s.stream, (uint8_t *)recd, !direct,
+		    (uint8_t *)seal)) != 0)
 			return rc;
+		sealed = seal != nullptr;
 	}
 	FI_POINT(FI_RECORD);
 	HIP_TRY(hipEventRecord(s.done, s.stream));
 	s.busy = true;
 	const bool tx = hb.tx;
-	const int dl = tx && hb.hash_alg != NET2_HASH_NIL ?
+	/* dl != 0: records to scatter (keyed TX, not sealed by the kernel) */
+	const int dl = tx && hb.hash_alg != NET2_HASH_NIL && !sealed ?
 	    digest_len(hb.hash_alg) : 0;
 	WorkPool *pp = &pool;
 	s.finish = [=]() {
@@ -2246,7 +2268,7 @@ int enqueue_burst_steps(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 			memcpy(hb.result + lo, st_res, (size_t)n);
 		for (const std::function<void()> &c : copies)
 			c();
-		if (!tx)
+		if (!tx || sealed)
 			return 0;
 		/* TX: the code of every datagram, and the sealed header (and
 		 * hash field) of every OK one into the caller's slot
