@@ -4,7 +4,8 @@ to stderr) of one RX and one TX host burst of 1 M MTU datagrams from pinned
 memory, after a warm-up call each: where a call's time goes chunk by chunk.
 
   NET2_SHA2_DEBUG_TIMING=1 python tools/burst_debug_timing.py [n]
-  REPS=20 python tools/burst_debug_timing.py     (call times only, back to back)
+  REPS=20 [ORDER=rx-first] python tools/burst_debug_timing.py
+                                     (call times only, back to back)
 """
 import ctypes
 import os
@@ -52,11 +53,24 @@ def main():
                                                    p(offs), p(lens), n, p(res), p(iv),
                                                    p(oseq), p(ofl), 1), "rx")
     reps = int(os.environ.get("REPS", "1"))
-    for name, fn in [("tx", tx), ("rx", rx)] + [("tx", tx)] * reps + [("rx", rx)] * reps:
+    seqs = [("tx", tx)] * reps + [("rx", rx)] * reps
+    if os.environ.get("ORDER") == "rx-first":
+        seqs = seqs[reps:] + seqs[:reps]
+    def throttled():
+        """The cgroup's CPU throttling counters (cgroup v2), if readable."""
+        try:
+            st = dict(ln.split() for ln in open("/sys/fs/cgroup/cpu.stat"))
+            return f"nr_throttled {st.get('nr_throttled')} " \
+                   f"throttled_usec {st.get('throttled_usec')} usage_usec {st.get('usage_usec')}"
+        except (OSError, ValueError):
+            return "cpu.stat n/a"
+    print("cpu.max:", open("/sys/fs/cgroup/cpu.max").read().strip()
+          if os.path.exists("/sys/fs/cgroup/cpu.max") else "n/a", file=sys.stderr)
+    for name, fn in [("tx", tx), ("rx", rx)] + seqs:
         t0 = time.perf_counter()
         fn()
-        print(f"== {name} {n} datagrams: {(time.perf_counter() - t0) * 1e3:.3f} ms",
-              file=sys.stderr, flush=True)
+        print(f"== {name} {n} datagrams: {(time.perf_counter() - t0) * 1e3:.3f} ms  "
+              f"[{throttled()}]", file=sys.stderr, flush=True)
 
 
 if __name__ == "__main__":
