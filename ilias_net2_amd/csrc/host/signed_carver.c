@@ -131,6 +131,7 @@ pool_worker(void *unused)
 	struct sc_task t;
 
 	(void)unused;
+	pthread_setname_np(pthread_self(), "net2-sc");
 	pthread_mutex_lock(&g_pool.mu);
 	for (;;) {
 		while (!pool_pop(&t))

@@ -295,9 +295,16 @@ struct Slot {
  * Host worker threads for packing staged chunks, kept alive between chunks
  * and calls: spawning and joining 16 threads twice per 64 MiB chunk cost
  * about a third of the pack itself.  run(nt, f) calls f(0) on the caller and
- * f(1..nt-1) on workers and returns when all are done.  Workers spin for
- * about half a millisecond after a job (the next chunk's job usually comes
- * sooner), then sleep on a condition variable.  The job word packs the
+ * f(1..nt-1) on workers and returns when all are done.  Workers that took
+ * part in a job spin for about half a millisecond after it, the others for
+ * 50 us after seeing one (a chunk runs a small job and then a full-width
+ * one back to back), then sleep on a condition variable: every worker
+ * spinning half a millisecond after every job burnt ~6 CPUs during a 1
+ * M-datagram host burst (tools/burst_debug_timing.py), none spinning after
+ * a job it sat out cost the pageable host bursts 8-40 % (the full-width
+ * pack waited for sleeping workers).  This way: ~34 ms of CPU per 1 M
+ * datagrams against ~105, call times the same or better
+ * (profiles/round6/spin_ab/).  The job word packs the
  * generation with nt, so a worker that wakes late never runs a job it is
  * not counted in.  Pools are never destroyed (their threads are detached
  * and may be parked at process exit).  One job at a time: job_, pending_
@@ -307,6 +314,9 @@ struct Slot {
  */
 #ifndef NET2_POOL_SPIN_US
 #define NET2_POOL_SPIN_US 500
+#endif
+#ifndef NET2_POOL_SPIN_IDLE_US
+#define NET2_POOL_SPIN_IDLE_US 50
 #endif
 
 class WorkPool {
@@ -348,14 +358,19 @@ private:
 
 	void worker(size_t idx, uint64_t seen)
 	{
+		/* named, so per-thread CPU time can be told apart
+		 * (/proc/<pid>/task/<tid>/comm, tools/burst_debug_timing.py) */
+		pthread_setname_np(pthread_self(), "net2-pack");
+		bool ran = false;	/* took part in the last job */
 		for (;;) {
 			uint64_t w = seen;
 			const double t0 = dbg_clock();
+			const double spin_ms = (ran ? NET2_POOL_SPIN_US :
+			    NET2_POOL_SPIN_IDLE_US) * 1e-3;
 			for (unsigned i = 1; w == seen; i++) {
 				__builtin_ia32_pause();
 				w = word_.load(std::memory_order_acquire);
-				if ((i & 1023) == 0 &&
-				    dbg_clock() - t0 > NET2_POOL_SPIN_US * 1e-3)
+				if ((i & 255) == 0 && dbg_clock() - t0 > spin_ms)
 					break;
 			}
 			if (w == seen) {
@@ -367,7 +382,8 @@ private:
 				w = word_.load(std::memory_order_acquire);
 			}
 			seen = w;
-			if (idx < (w & 0xff)) {
+			ran = idx < (w & 0xff);
+			if (ran) {
 				(*job_)(idx);
 				pending_.fetch_sub(1, std::memory_order_release);
 			}
@@ -1032,6 +1048,7 @@ public:
 private:
 	void loop()
 	{
+		pthread_setname_np(pthread_self(), "net2-slice");
 		for (;;) {
 			std::function<void()> f;
 			{

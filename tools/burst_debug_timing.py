@@ -64,13 +64,39 @@ def main():
                    f"throttled_usec {st.get('throttled_usec')} usage_usec {st.get('usage_usec')}"
         except (OSError, ValueError):
             return "cpu.stat n/a"
+    def thread_cpu():
+        """CPU seconds of this process's threads, by thread name."""
+        tick = os.sysconf("SC_CLK_TCK")
+        by = {}
+        for tid in os.listdir("/proc/self/task"):
+            try:
+                name = open(f"/proc/self/task/{tid}/comm").read().strip()
+                f = open(f"/proc/self/task/{tid}/stat").read().rsplit(")", 1)[1].split()
+                by[name] = by.get(name, 0.0) + (int(f[11]) + int(f[12])) / tick
+            except (OSError, ValueError, IndexError):
+                pass
+        return by
+
+    def cpu_report(label, a, b, calls):
+        rows = sorted(((b.get(k, 0.0) - a.get(k, 0.0), k) for k in b), reverse=True)
+        txt = ", ".join(f"{k} {d * 1e3 / calls:.1f}" for d, k in rows if d > 0)
+        print(f"-- CPU ms per call by thread, {label}: {txt}", file=sys.stderr)
     print("cpu.max:", open("/sys/fs/cgroup/cpu.max").read().strip()
           if os.path.exists("/sys/fs/cgroup/cpu.max") else "n/a", file=sys.stderr)
-    for name, fn in [("tx", tx), ("rx", rx)] + seqs:
+    prev, cur_kind, ncalls = None, None, 0
+    for k, (name, fn) in enumerate([("tx", tx), ("rx", rx)] + seqs):
+        if k >= 2 and name != cur_kind:
+            now = thread_cpu()
+            if prev is not None:
+                cpu_report(cur_kind, prev, now, ncalls)
+            prev, cur_kind, ncalls = now, name, 0
         t0 = time.perf_counter()
         fn()
+        ncalls += 1
         print(f"== {name} {n} datagrams: {(time.perf_counter() - t0) * 1e3:.3f} ms  "
               f"[{throttled()}]", file=sys.stderr, flush=True)
+    if prev is not None:
+        cpu_report(cur_kind, prev, thread_cpu(), ncalls)
 
 
 if __name__ == "__main__":
