@@ -315,6 +315,11 @@ struct Slot {
 #ifndef NET2_POOL_SPIN_US
 #define NET2_POOL_SPIN_US 500
 #endif
+/* keyed host bursts of at most this many datagrams read their datagrams and
+ * metadata through the host mapping (enqueue_burst_steps) */
+#ifndef NET2_BURST_ZC_MAX
+#define NET2_BURST_ZC_MAX 16384
+#endif
 #ifndef NET2_POOL_SPIN_IDLE_US
 #define NET2_POOL_SPIN_IDLE_US 50
 #endif
@@ -2151,7 +2156,32 @@ int enqueue_burst_steps(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 	const size_t bytes = direct ? re - rs : plan.start[plan.nt];
 	if ((rc = s.reserve(bytes, n)) != 0)
 		return rc;
-	const BurstSlot::Meta hm(s.h_meta, n), dm(s.d_meta, n);
+	/*
+	 * A small keyed burst (the one-launch form): its kernel reads the
+	 * datagrams and their metadata through their host mapping -- the
+	 * caller's page-locked buffer or the slot's staging -- instead of
+	 * waiting for two copies: 5-13 % faster from 64 to 16,384 datagrams,
+	 * RX and TX, pinned and pageable (profiles/round6/zc_ab/, three
+	 * alternations in flipped order).
+	 */
+	const bool keyed = hb.tx ? hb.hash_alg != NET2_HASH_NIL :
+	    hb.keys->hash_alg != NET2_HASH_NIL;
+	uint8_t *z_in = nullptr, *z_meta = nullptr;
+	if (keyed && n <= NET2_BURST_ZC_MAX && n <= net2_burst_wave_max()) {
+		void *a = nullptr, *m = nullptr;
+		if (hipHostGetDevicePointer(&a, direct ? (void *)(hb.base + rs) :
+		    (void *)s.h_in, 0) == hipSuccess && a != nullptr &&
+		    hipHostGetDevicePointer(&m, s.h_meta, 0) == hipSuccess &&
+		    m != nullptr) {
+			z_in = (uint8_t *)a;
+			z_meta = (uint8_t *)m;
+		} else {
+			(void)hipGetLastError();
+		}
+	}
+	uint8_t *const d_in = z_in != nullptr ? z_in : s.d_in;
+	const BurstSlot::Meta hm(s.h_meta, n),
+	    dm(z_meta != nullptr ? z_meta : s.d_meta, n);
 	if (direct) {
 		/* the chunk's datagrams lie densely in one page-locked
 		 * allocation: copied as they lie, no host pack */
@@ -2167,7 +2197,7 @@ int enqueue_burst_steps(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 				hl[j] = ln[j];
 			}
 		});
-		if (bytes != 0)
+		if (bytes != 0 && z_in == nullptr)
 			HIP_TRY(hipMemcpyAsync(s.d_in, hb.base + rs, bytes,
 			    hipMemcpyHostToDevice, s.stream));
 		if (dbg_timing())
@@ -2179,7 +2209,7 @@ int enqueue_burst_steps(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 		if (dbg_timing())
 			fprintf(stderr, "net2 burst: pack %zu B: %.3f ms (%zu "
 			    "threads)\n", bytes, dbg_now() - tp0, plan.nt);
-		if (bytes != 0)
+		if (bytes != 0 && z_in == nullptr)
 			HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, bytes,
 			    hipMemcpyHostToDevice, s.stream));
 	}
@@ -2188,8 +2218,10 @@ int enqueue_burst_steps(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 		memcpy(hm.hdr + n, hb.flags_in + lo, (size_t)n * 4);
 	}
 	/* offsets, lengths (and TX headers): one copy */
-	HIP_TRY(hipMemcpyAsync(s.d_meta, s.h_meta,
-	    BurstSlot::meta_bytes(n, hb.tx), hipMemcpyHostToDevice, s.stream));
+	if (z_meta == nullptr)
+		HIP_TRY(hipMemcpyAsync(s.d_meta, s.h_meta,
+		    BurstSlot::meta_bytes(n, hb.tx), hipMemcpyHostToDevice,
+		    s.stream));
 	FI_POINT(FI_H2D);
 
 	/* staged results: [code n][IV n x ivlen | records][seq n][flags n] */
@@ -2216,7 +2248,7 @@ int enqueue_burst_steps(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 		    nullptr || (k_fl = out_ptr(hb.flags_out + lo, pins.flags,
 		    st_fl, &c_fl)) == nullptr))
 			return EIO;
-		if ((rc = decode_burst(hb.keys, hb.ivlen, s.d_in, dm.off, dm.len,
+		if ((rc = decode_burst(hb.keys, hb.ivlen, d_in, dm.off, dm.len,
 		    n, k_res, k_iv, (uint32_t *)k_sq, (uint32_t *)k_fl, s.d_ws,
 		    s.stream, true)) != 0)
 			return rc;
@@ -2230,7 +2262,6 @@ int enqueue_burst_steps(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 			copies.push_back([=]() { memcpy(hb.flags_out + lo, st_fl,
 			    (size_t)n * 4); });
 	} else {
-		const bool keyed = hb.hash_alg != NET2_HASH_NIL;
 		/*
 		 * Datagrams copied as they lie from one page-locked allocation:
 		 * the kernel seals headers and hash fields straight into the
@@ -2266,7 +2297,7 @@ int enqueue_burst_steps(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 		 * measured 1.5 % slower (binoff_*.jsonl).
 		 */
 		if ((rc = encode_burst(hb.hash_alg, hb.hash_key, hb.hash_keylen,
-		    hb.enc_alg, dm.hdr, dm.hdr + n, s.d_in, dm.off, dm.len, n,
+		    hb.enc_alg, dm.hdr, dm.hdr + n, d_in, dm.off, dm.len, n,
 		    k_res, s.d_ws, s.stream, (uint8_t *)recd, !direct,
 		    (uint8_t *)seal)) != 0)
 			return rc;
