@@ -15,13 +15,18 @@
  *                             coalescer);
  * then the argument checks (EINVAL before any device work).
  * Prints "host_asan ok" and exits 0 when everything matched; ASan aborts
- * the process on a heap, stack or global overflow or a use after free.
+ * the process on a heap, stack or global overflow or a use after free.  A
+ * watchdog reports each single-call thread's last call and exits 3 if the
+ * single calls take more than 20 s.
  *
  *   NET2_SHA2_VIRTUAL_DEVICES=3 ./host_asan   also runs the sharded paths
  */
 #include <hip/hip_runtime_api.h>
 
+#include <atomic>
 #include <cerrno>
+#include <chrono>
+#include <unistd.h>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -115,6 +120,8 @@ static void batch_case(int alg, bool var, uint64_t n, uint32_t maxlen, bool pin)
 
 static void burst_case(int hash_alg, bool enc, uint32_t ivlen, uint64_t n, bool pin)
 {
+	fprintf(stderr, "burst alg %d n %llu pin %d\n", hash_alg,
+	    (unsigned long long)n, pin);
 	const uint32_t hl = (uint32_t)dlen_of(hash_alg - 3);
 	std::vector<uint32_t> seq(n ? n : 1), fl(n ? n : 1), slot(n ? n : 1);
 	std::vector<uint64_t> offs(n ? n : 1);
@@ -170,6 +177,7 @@ static void burst_case(int hash_alg, bool enc, uint32_t ivlen, uint64_t n, bool 
 	k.hash_key = key.data();
 	k.hash_keylen = hl;
 	k.enc_alg = enc ? 1 : 0;
+	fprintf(stderr, "  tx ok, rx\n");
 	rc = net2_packet_decode_burst_host(&k, ivlen, buf.p, offs.data(),
 	    lens.data(), n, r2.p, ivlen ? iv.p : nullptr, s2.p, f2.p, 0);
 	CHECK(rc == 0, "decode_burst_host n %llu: rc %d", (unsigned long long)n, rc);
@@ -190,10 +198,31 @@ static void burst_case(int hash_alg, bool enc, uint32_t ivlen, uint64_t n, bool 
 	    (unsigned long long)bad, (unsigned long long)n, pin);
 }
 
+/* what each single-call thread is doing (a watchdog reports it if the
+ * calls do not finish) */
+static std::atomic<int> sc_state[8][3];	/* call index, alg, length */
+static std::atomic<bool> sc_done{false};
+
 static void single_calls()
 {
 	std::vector<std::thread> th;
 	std::vector<int> bad(8, 0);
+	std::thread dog([] {
+		for (int i = 0; i < 400 && !sc_done.load(); i++)
+			std::this_thread::sleep_for(std::chrono::milliseconds(50));
+		if (sc_done.load())
+			return;
+		uint64_t calls = 0, launches = 0;
+		net2_coalesce_stats(0, &calls, &launches);
+		fprintf(stderr, "watchdog: single calls not done after 20 s; "
+		    "coalescer calls %llu launches %llu\n",
+		    (unsigned long long)calls, (unsigned long long)launches);
+		for (int t = 0; t < 8; t++)
+			fprintf(stderr, "  thread %d: call %d alg %d len %d\n", t,
+			    sc_state[t][0].load(), sc_state[t][1].load(),
+			    sc_state[t][2].load());
+		_exit(3);
+	});
 	for (int t = 0; t < 8; t++)
 		th.emplace_back([t, &bad] {
 			uint64_t s = 0x1234567ull * (t + 1);
@@ -212,6 +241,9 @@ static void single_calls()
 				struct iovec iov[2] = {{m.data(), cut}, {m.data() + cut, len - cut}};
 				uint8_t out[64], want[64];
 				const bool hm = alg > 3;
+				sc_state[t][0] = c;
+				sc_state[t][1] = alg;
+				sc_state[t][2] = (int)len;
 				int rc = net2_hashctx_hashiov(alg, hm ? key.data() : nullptr,
 				    hm ? key.size() : 0, iov, 2, out, sizeof(out));
 				int dl = hm ? oracle_hmac_digest(alg, key.data(), key.size(),
@@ -222,6 +254,8 @@ static void single_calls()
 		});
 	for (auto &x : th)
 		x.join();
+	sc_done = true;
+	dog.join();
 	int sum = 0;
 	for (int b : bad)
 		sum += b;
