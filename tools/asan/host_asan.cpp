@@ -1,6 +1,6 @@
 /*
  * host_asan -- the host side of libnet2_sha2 under AddressSanitizer (test
- * infrastructure, built by tests/asan/Makefile: every object of the library
+ * infrastructure, built by tools/asan/Makefile: every object of the library
  * recompiled with ASan on the host code only, the device code unchanged,
  * linked into this executable together with the CPU oracle as the checker).
  *
