@@ -680,11 +680,14 @@ struct PackPlan {
 	size_t start[kPackThreads + 1] = {};	/* start[nt] = total bytes */
 };
 
-PackPlan pack_sizes(WorkPool &pool, const uint32_t *lens, uint64_t n)
+PackPlan pack_sizes(WorkPool &pool, const uint32_t *lens, uint64_t n,
+    int per_shift = 12)
 {
 	PackPlan pl;
-	/* one thread per ~4k packets (the fill copies ~MiBs each) */
-	pl.nt = std::min<size_t>(kPackThreads, std::max<size_t>(1, n >> 12));
+	/* one thread per 2^per_shift packets: ~4 K by default (the fill copies
+	 * ~MiBs each) */
+	pl.nt = std::min<size_t>(kPackThreads, std::max<size_t>(1,
+	    n >> per_shift));
 	size_t *st = pl.start;
 	const size_t nt = pl.nt;
 	pool.run(nt, [=](size_t t) {
@@ -2152,7 +2155,10 @@ int enqueue_burst_steps(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 	    &re);
 	PackPlan plan;
 	if (!direct)
-		plan = pack_sizes(pool, hb.lens + lo, n);
+		/* RX packs with a thread per ~1 K datagrams: 11-14 % faster
+		 * decode calls from 4,096 datagrams up; TX measured 15-18 %
+		 * slower that way and keeps ~4 K (profiles/round6/pack_ab/) */
+		plan = pack_sizes(pool, hb.lens + lo, n, hb.tx ? 12 : 10);
 	const size_t bytes = direct ? re - rs : plan.start[plan.nt];
 	if ((rc = s.reserve(bytes, n)) != 0)
 		return rc;
