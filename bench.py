@@ -883,6 +883,8 @@ def finalize_line(line):
             st = r.get("stages", {})
             b = {s: st[s].get("ms") for s in ("gpu_digest_sha512", "cpu_digest_sha512_1core",
                                                "sc_hash_tick") if s in st}
+        if k == "burst_small" and isinstance(r, dict):
+            b = {kk: r[kk] for kk in ("rx", "tx") if kk in r}
         if b:
             summary[k] = b
     out["summary"] = summary
@@ -929,7 +931,71 @@ def extra_configs(args, dev, probe, ws=1, rank=0, label=None):
         pg = burst_e2e_rate(kind, steps=4, warmup=1, memory="pageable")
         r["pageable"] = {k: pg[k] for k in ("value", "ms_per_step", "h2d_GBps")}
         out[f"burst_{kind}_e2e"] = r
+    out["burst_small"] = burst_small_latency()
     out["c1"] = run_c1()
+    return out
+
+
+def burst_small_latency(sizes=(64, 1024, 4096), budget_s=0.3):
+    """The integration's operating point (a receive loop
+    hands over whatever the socket holds, NET2_BURST 4,096): median time of
+    one net2_packet_decode_burst_host / _encode_burst_host call of 64 /
+    1,024 / 4,096 {136, 584, 1500}-byte HMAC-SHA512 datagrams with 16-byte
+    IVs from pinned host memory, one GPU, after two warm-up calls; every
+    call's codes checked (DESIGN.md §6.4 has the whole table and the CPU
+    beside it)."""
+    import ctypes
+    import statistics
+    import numpy as np
+    import torch
+    from ilias_net2_amd import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(11)
+    nmax = max(sizes)
+    lens_all = rng.choice(np.array([136, 584, 1500], dtype=np.uint32), nmax)
+    key = HMAC_KEY[:64]
+    kb = ctypes.create_string_buffer(key, 64)
+    keys = _lib.BurstRxKeys(6, ctypes.cast(kb, ctypes.c_void_p), 64, 1, None, 0, 0, 0, 0)
+
+    def pinned(shape, dt=torch.uint8):
+        return torch.empty(shape, dtype=dt, pin_memory=True).numpy()
+    p = lambda a: a.ctypes.data  # noqa: E731
+    out = {"unit": "us per call (median)", "memory": "pinned",
+           "workload": "HMAC-SHA512 + 16-byte IVs, {136, 584, 1500} B datagrams"}
+    for kind in ("rx", "tx"):
+        row = {}
+        for n in sizes:
+            lens = lens_all[:n].copy()
+            offs = np.zeros(n, dtype=np.uint64)
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+            data = pinned((int(lens.sum()),))
+            data[:] = rng.integers(0, 256, data.size, dtype=np.uint8)
+            res, iv = pinned((n,)), pinned((n, 16))
+            oseq, ofl = pinned((n,), torch.int32), pinned((n,), torch.int32)
+            seq = np.arange(n, dtype=np.uint32)
+            flags = np.full(n, 3, dtype=np.uint32)
+
+            def tx():
+                _lib.check(L.net2_packet_encode_burst_host(
+                    6, key, 64, 1, p(seq), p(flags), p(data), p(offs), p(lens), n,
+                    p(res), 1), "net2_packet_encode_burst_host")
+
+            def rx():
+                _lib.check(L.net2_packet_decode_burst_host(
+                    ctypes.byref(keys), 16, p(data), p(offs), p(lens), n, p(res), p(iv),
+                    p(oseq), p(ofl), 1), "net2_packet_decode_burst_host")
+            tx()                                # sealed once, then timed
+            fn = rx if kind == "rx" else tx
+            fn()
+            fn()
+            ts, t_all = [], time.perf_counter()
+            while len(ts) < 400 and (time.perf_counter() - t_all < budget_s or len(ts) < 20):
+                t0 = time.perf_counter()
+                fn()
+                ts.append(time.perf_counter() - t0)
+            assert int((res != 0).sum()) == 0, f"burst_small {kind} {n}: not OK"
+            row[str(n)] = round(statistics.median(ts) * 1e6, 1)
+        out[kind] = row
     return out
 
 
