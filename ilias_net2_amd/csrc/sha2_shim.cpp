@@ -2155,10 +2155,12 @@ int enqueue_burst_steps(WorkPool &pool, BurstSlot &s, const HostBurst &hb,
 	    &re);
 	PackPlan plan;
 	if (!direct)
-		/* RX packs with a thread per ~1 K datagrams: 11-14 % faster
-		 * decode calls from 4,096 datagrams up; TX measured 15-18 %
-		 * slower that way and keeps ~4 K (profiles/round6/pack_ab/) */
-		plan = pack_sizes(pool, hb.lens + lo, n, hb.tx ? 12 : 10);
+		/* RX packs with a thread per ~512 datagrams: 10-12 % faster
+		 * decode calls from 4,096 datagrams up than per ~4 K, 1-4 %
+		 * faster again than per ~1 K from 1,024 to 4,096; TX measured
+		 * 15-18 % slower per ~1 K and keeps ~4 K
+		 * (profiles/round6/pack_ab/) */
+		plan = pack_sizes(pool, hb.lens + lo, n, hb.tx ? 12 : 9);
 	const size_t bytes = direct ? re - rs : plan.start[plan.nt];
 	if ((rc = s.reserve(bytes, n)) != 0)
 		return rc;
